@@ -1,0 +1,141 @@
+/*
+ * rt_mi355x.h — C ABI of the MI355X-native Monte-Carlo sample loop.
+ *
+ * Drop-in boundary for semicolonTransistor/rust-ray-tracing's hot path:
+ *   trait Renderer { fn render(&self, max_bounces, samples_per_pixel, &Arc<Scene>, &Arc<Camera>)
+ *                    -> (RgbImage, RenderStat) }                     (src/renderer.rs:38-40)
+ * whose live implementation is TileRenderer::render (src/renderer.rs:243-387) driving
+ * TileRenderTask::render_vectorized2 (src/renderer.rs:141-176) ->
+ * Scene::trace_vectorized2 (src/ray_tracing.rs:375-505).  A GPU renderer is a new
+ * `impl Renderer` that flattens Scene/Camera into the structs below and calls rt_render
+ * (or the device-resident rt_context_* API); the Rust-side binding is in INTEGRATION.md.
+ *
+ * Everything is plain C: pointers + sizes, caller-owned buffers, int status codes.
+ * Thread-safety: rt_render may be called from any thread; one rt_context must not be
+ * used concurrently from two threads.
+ */
+#ifndef RT_MI355X_H
+#define RT_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (the reference panics instead; see rt_last_error) ---- */
+#define RT_OK 0
+#define RT_ERR_INVALID 1     /* bad argument: NULL pointer, spp == 0, material index out of range ...
+                                (reference: unwrap()/panic!, e.g. objects.rs:296, materials.rs:31) */
+#define RT_ERR_HIP 2         /* HIP runtime failure (no device, launch failure, OOM) */
+#define RT_ERR_RANGE 3       /* a pixel channel exceeded 2.0 after /spp: the reference panics in
+                                Color::to_u8_array (color.rs:55-57); the image is still written */
+#define RT_ERR_UNSUPPORTED 4 /* configuration this build cannot run (e.g. spp beyond the LDS budget) */
+
+/* ---- materials (src/materials.rs:41-155) ---- */
+#define RT_LAMBERTIAN 0u
+#define RT_METAL 1u
+#define RT_DIELECTRIC 2u
+
+typedef struct rt_material {
+    uint32_t kind;       /* RT_LAMBERTIAN / RT_METAL / RT_DIELECTRIC */
+    uint32_t hollow;     /* Dielectric::hollow (materials.rs:111-114) */
+    double albedo[3];    /* Lambertian::albedo / Metal::albedo */
+    double fuzz;         /* Metal::fuzzy_factor, already clamped by Metal::new (materials.rs:79-88) */
+    double ior;          /* Dielectric::index_of_refraction */
+} rt_material;           /* 48 bytes */
+
+/* ---- scene: spheres in scene order (closest-hit ties resolve to the later sphere,
+ *      objects.rs:141), Scene::objects (ray_tracing.rs:102-104) flattened SoA ---- */
+typedef struct rt_scene {
+    uint32_t n_spheres;
+    uint32_t n_materials;
+    const double* center;         /* [n_spheres][3] */
+    const double* radius;         /* [n_spheres] */
+    const uint32_t* material;     /* [n_spheres], index into materials */
+    const rt_material* materials; /* [n_materials] */
+} rt_scene;
+
+/* ---- camera: the precomputed fields of Camera (ray_tracing.rs:15-24) ---- */
+typedef struct rt_camera {
+    uint32_t image_width, image_height;
+    double center[3];   /* Camera::center */
+    double ulc[3];      /* Camera::viewport_upper_left_corner */
+    double vu[3];       /* Camera::viewport_u */
+    double vv[3];       /* Camera::viewport_v */
+    double du[3];       /* Camera::defocus_u */
+    double dv[3];       /* Camera::defocus_v */
+} rt_camera;
+
+/* Pixel set to render: rows row_begin + i*row_step (i < row_count), columns
+ * [col_begin, col_begin + col_count).  Outputs are compact over the set:
+ * element (i, c) at index i*col_count + c.  NULL = whole image (== RgbImage layout). */
+typedef struct rt_tile_range {
+    uint32_t row_begin, row_step, row_count;
+    uint32_t col_begin, col_count;
+} rt_tile_range;
+
+/* RenderStat (renderer.rs:11-34) plus the work counters the roofline needs. */
+typedef struct rt_stats {
+    double seconds;          /* wall time of the call (host clock) */
+    double kernel_ms;        /* device time of the trace kernel(s), HIP events */
+    double pixels_per_second;
+    uint64_t pixels;
+    uint64_t samples;        /* pixels * spp */
+    uint64_t ray_segments;   /* enabled rays traced, summed over bounces (ray_tracing.rs:396-401) */
+} rt_stats;
+
+/* ---- flags ---- */
+#define RT_FLAG_F32 0x1u     /* compute in fp32 (default: fp64, the reference's arithmetic) */
+#define RT_FLAG_ROOT2 0x2u   /* quirk Q1 off: accept the far root like scalar Sphere::hit
+                                (objects.rs:228-234) instead of testing root1 twice (objects.rs:273) */
+
+/* Camera::new (ray_tracing.rs:27-62).  view_angle and defocus_angle in degrees. */
+int rt_camera_new(rt_camera* out, uint32_t image_width, uint32_t image_height, double focal_length,
+                  double view_angle_deg, const double center[3], const double look_at[3],
+                  const double up[3], double defocus_angle_deg);
+
+/* Metal::new's clamp (materials.rs:79-88): fuzz < 1 ? fuzz : 1. */
+double rt_metal_clamp_fuzz(double fuzz);
+
+/* One-shot render, host buffers in/out (replaces TileRenderer::render, renderer.rs:243-387,
+ * on the device; scene upload and PCIe copies included).
+ *   rgb8:   [pixels][3] RGB8, Color::to_u8_array of (sum / spp)   (may be NULL)
+ *   linear: [pixels][3] f64 pixel colour after /spp, before gamma (may be NULL)
+ *   stats:  may be NULL
+ * Returns RT_OK, RT_ERR_RANGE (image written; reference would have panicked) or an error. */
+int rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
+              uint64_t seed, uint32_t flags, const rt_tile_range* range, uint8_t* rgb8,
+              double* linear, rt_stats* stats);
+
+/* ---- device-resident API: scene kept in HBM across calls, outputs in device memory ---- */
+typedef struct rt_context rt_context;
+
+int rt_context_create(int device, rt_context** out);
+int rt_context_destroy(rt_context* ctx);
+/* Upload (replace) the scene; copies fp64 and fp32 SoA images into HBM. */
+int rt_context_set_scene(rt_context* ctx, const rt_scene* scene);
+/* Enqueue one render on `stream` (hipStream_t, NULL = the context's own stream).
+ * d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous. */
+int rt_render_async(rt_context* ctx, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
+                    uint64_t seed, uint32_t flags, const rt_tile_range* range, void* d_rgb8,
+                    void* d_linear, void* stream);
+/* Synchronise `stream`, then report and reset the counters accumulated by the renders
+ * enqueued since the last call (ray_segments, error flag).  kernel_ms = device time between
+ * the first and last enqueued render (HIP events on that stream). */
+int rt_context_collect(rt_context* ctx, void* stream, rt_stats* stats);
+/* Device memory helpers (so hosts without a HIP toolchain can drive the async API). */
+int rt_device_alloc(rt_context* ctx, size_t bytes, void** out);
+int rt_device_free(rt_context* ctx, void* ptr);
+int rt_memcpy_d2h(rt_context* ctx, void* dst, const void* src, size_t bytes);
+
+/* Last error message of the calling thread ("" if none). */
+const char* rt_last_error(void);
+/* Build/version string, e.g. "rt_mi355x 0.1 gfx950". */
+const char* rt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT_MI355X_H */

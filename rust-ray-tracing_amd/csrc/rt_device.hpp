@@ -1,0 +1,140 @@
+// rt_device.hpp — device-side scalar math of the sample loop, generic over T = float | double.
+//
+// Every formula restates the reference's arithmetic (file:line cited) and must be compiled
+// with -ffp-contract=off: an fma appears exactly where the reference writes mul_add
+// (PackedVec3::length_squared / dot, geometry.rs:434-436,466-468; discriminant,
+// objects.rs:257).  Division and sqrt are the correctly-rounded IEEE ops (hipcc default for
+// f64; -fhip-fp32-correctly-rounded-divide-sqrt for f32), so the kernel computes the same
+// bits as the CPU restatement in oracle/ for the same (seed, pixel, sample).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rt {
+
+template <typename T> struct V3 { T x, y, z; };
+
+template <typename T> __device__ __forceinline__ V3<T> mk(T x, T y, T z) { return V3<T>{x, y, z}; }
+// Scalar Vec3 ops (geometry.rs:37-132): no FMA, sums left to right.
+template <typename T> __device__ __forceinline__ V3<T> add(V3<T> a, V3<T> b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+template <typename T> __device__ __forceinline__ V3<T> sub(V3<T> a, V3<T> b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+template <typename T> __device__ __forceinline__ V3<T> mul(V3<T> a, T s) { return mk(a.x * s, a.y * s, a.z * s); }
+template <typename T> __device__ __forceinline__ V3<T> dvs(V3<T> a, T s) { return mk(a.x / s, a.y / s, a.z / s); }
+template <typename T> __device__ __forceinline__ V3<T> neg(V3<T> a) { return mk(-a.x, -a.y, -a.z); }
+template <typename T> __device__ __forceinline__ T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+template <typename T> __device__ __forceinline__ T len2(V3<T> a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
+template <typename T> __device__ __forceinline__ V3<T> unit(V3<T> a) { return dvs(a, sqrt(len2(a))); }
+// Packed ops keep the reference's explicit FMA.
+template <typename T> __device__ __forceinline__ T pk_len2(V3<T> a) { return fma(a.z, a.z, fma(a.y, a.y, a.x * a.x)); }
+template <typename T> __device__ __forceinline__ T pk_dot(V3<T> a, V3<T> b) { return fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)); }
+
+// geometry.rs:134-137
+template <typename T> __device__ __forceinline__ bool near_zero(V3<T> v) {
+    const T e = T(1e-8);
+    return fabs(v.x) < e && fabs(v.y) < e && fabs(v.z) < e;
+}
+// geometry.rs:179-181
+template <typename T> __device__ __forceinline__ V3<T> reflect(V3<T> v, V3<T> n) { return sub(v, mul(n, T(2.0) * dot(v, n))); }
+// geometry.rs:183-188
+template <typename T> __device__ __forceinline__ V3<T> refract(V3<T> v, V3<T> n, T ratio) {
+    T ct = fmin(dot(neg(v), n), T(1.0));
+    V3<T> rperp = mul(add(v, mul(n, ct)), ratio);
+    V3<T> rpar = mul(n, -(sqrt(fabs(T(1.0) - len2(rperp)))));
+    return add(rperp, rpar);
+}
+
+// ---- counter-based RNG: Philox4x32-10 keyed by (sample, pixel, bounce, stream) ----
+struct U4 { uint32_t a, b, c, d; };
+__device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    return U4{c0, c1, c2, c3};
+}
+// Uniform [0,1): f64 from 53 bits of (a,b) / (c,d); f32 from 24 bits of a / b.
+__device__ __forceinline__ double u01a(const U4& r, double) { return (double)((((uint64_t)r.a << 32) | r.b) >> 11) * 0x1.0p-53; }
+__device__ __forceinline__ double u01b(const U4& r, double) { return (double)((((uint64_t)r.c << 32) | r.d) >> 11) * 0x1.0p-53; }
+__device__ __forceinline__ float u01a(const U4& r, float) { return (float)(r.a >> 8) * 0x1.0p-24f; }
+__device__ __forceinline__ float u01b(const U4& r, float) { return (float)(r.b >> 8) * 0x1.0p-24f; }
+
+// sin/cos(2*pi*u): exact quadrant reduction in u-space + Taylor on [0, pi/4] by fma-Horner.
+__device__ __forceinline__ void poly_sincos(double x2, double& ps, double& pc) {
+    ps = 1.0 / 355687428096000.0;
+    ps = fma(ps, x2, -1.0 / 1307674368000.0);
+    ps = fma(ps, x2, 1.0 / 6227020800.0);
+    ps = fma(ps, x2, -1.0 / 39916800.0);
+    ps = fma(ps, x2, 1.0 / 362880.0);
+    ps = fma(ps, x2, -1.0 / 5040.0);
+    ps = fma(ps, x2, 1.0 / 120.0);
+    ps = fma(ps, x2, -1.0 / 6.0);
+    pc = -1.0 / 6402373705728000.0;
+    pc = fma(pc, x2, 1.0 / 20922789888000.0);
+    pc = fma(pc, x2, -1.0 / 87178291200.0);
+    pc = fma(pc, x2, 1.0 / 479001600.0);
+    pc = fma(pc, x2, -1.0 / 3628800.0);
+    pc = fma(pc, x2, 1.0 / 40320.0);
+    pc = fma(pc, x2, -1.0 / 720.0);
+    pc = fma(pc, x2, 1.0 / 24.0);
+    pc = fma(pc, x2, -1.0 / 2.0);
+}
+__device__ __forceinline__ void poly_sincos(float x2, float& ps, float& pc) {
+    ps = (float)(1.0 / 362880.0);
+    ps = fmaf(ps, x2, (float)(-1.0 / 5040.0));
+    ps = fmaf(ps, x2, (float)(1.0 / 120.0));
+    ps = fmaf(ps, x2, (float)(-1.0 / 6.0));
+    pc = (float)(-1.0 / 3628800.0);
+    pc = fmaf(pc, x2, (float)(1.0 / 40320.0));
+    pc = fmaf(pc, x2, (float)(-1.0 / 720.0));
+    pc = fmaf(pc, x2, (float)(1.0 / 24.0));
+    pc = fmaf(pc, x2, (float)(-1.0 / 2.0));
+}
+template <typename T> __device__ __forceinline__ void sincos2pi(T u, T& so, T& co) {
+    const T t = u * T(4.0);
+    const int q = (int)t;
+    const T f = t - (T)q;
+    const bool sw = f > T(0.5);
+    const T g = sw ? T(1.0) - f : f;
+    const T x = g * T(1.5707963267948966);
+    const T x2 = x * x;
+    T ps, pc;
+    poly_sincos(x2, ps, pc);
+    T s = fma(x * x2, ps, x);
+    T c = fma(x2, pc, T(1.0));
+    if (sw) { const T tmp = s; s = c; c = tmp; }
+    switch (q & 3) {
+        case 0: so = s; co = c; break;
+        case 1: so = c; co = -s; break;
+        case 2: so = -s; co = -c; break;
+        default: so = -c; co = s; break;
+    }
+}
+// Uniform direction on S^2: the distribution of Vec3::random_unit_vector (geometry.rs:139-152).
+template <typename T> __device__ __forceinline__ V3<T> unit_vec(T u1, T u2) {
+    const T z = T(1.0) - T(2.0) * u1;
+    const T r = sqrt(T(1.0) - z * z);
+    T s, c;
+    sincos2pi(u2, s, c);
+    return mk(r * c, r * s, z);
+}
+
+// Sky gradient of trace_vectorized2's final pass (ray_tracing.rs:490-494).
+template <typename T> __device__ __forceinline__ V3<T> sky(T y) {
+    const T a = (y + T(1.0)) * T(0.5);
+    const T oma = -a + T(1.0);
+    return mk(T(1.0) * oma + T(0.5) * a, T(1.0) * oma + T(0.7) * a, T(1.0) * oma + T(1.0) * a);
+}
+
+// Color::to_u8_array (color.rs:54-64): sqrt gamma, *255.999, saturating `as u8` (NaN -> 0).
+template <typename T> __device__ __forceinline__ uint8_t q8(T v) {
+    const T x = sqrt(v) * T(255.999);
+    if (!(x > T(0.0))) return 0;
+    if (x >= T(255.0)) return 255;
+    return (uint8_t)x;
+}
+
+}  // namespace rt

@@ -1,0 +1,626 @@
+// rt_kernel.hip — MI355X (gfx950) megakernel for the reference's per-pixel sample loop.
+//
+// Replaces TileRenderTask::render_vectorized2 (src/renderer.rs:141-176) and everything it
+// calls: Camera::get_ray (ray_tracing.rs:77-89), Scene::trace_vectorized2
+// (ray_tracing.rs:375-505), Sphere::hit_packed (objects.rs:249-290), PackedHitRecords
+// (objects.rs:121-176), Material::get_hit_result (materials.rs:54-147), the final sky pass and
+// reduction (ray_tracing.rs:486-504), /spp and Color::to_u8_array (renderer.rs:161,
+// color.rs:54-64).
+//
+// Mapping (one workgroup per pixel, wave64):
+//   * the pixel's spp samples are P = 4*ceil(spp/4) logical *positions* (the reference's
+//     C chunks x 4 lanes).  Active rays always occupy positions [0, n_k); position p lives
+//     on thread p % NT, slot p / NT, so n_k active rays occupy ceil(n_k/64) waves.
+//   * per bounce each active ray is traced against every sphere (sphere SoA read through
+//     the scalar cache: every lane of the wave tests the same sphere, operands in SGPRs);
+//   * survivors are compacted stably (the reference's shuffle, ray_tracing.rs:430-481) by
+//     __ballot + mbcnt + a cross-wave prefix over LDS counters, and their state moves to the
+//     new position in LDS, so the next bounce runs on dense waves;
+//   * quirk Q3 (the final read of buffer (C-1)%2, ray_tracing.rs:486) is reproduced without
+//     the second buffer: each position's final value is fixed at its retire bounce
+//     ("retire rule") and stored in an LDS array indexed by position; the
+//     final sum walks that array in the reference's order (per lane over chunks, then lanes),
+//     so fp64 results are bit-identical to the CPU restatement.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <chrono>
+#include <cmath>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_mi355x.h"
+#include "rt_device.hpp"
+
+namespace rt {
+
+template <typename T> struct MatT {
+    uint32_t kind, hollow;
+    T ar, ag, ab, fuzz, ior;
+};
+
+template <typename T> struct KParams {
+    const T* sph;              // [n][4] = cx, cy, cz, r*r (r.powi(2), objects.rs:256) in T
+    const uint32_t* smat;      // [n] material index
+    const MatT<T>* mats;
+    uint32_t n_spheres;
+    uint32_t W, H;
+    T center[3], ulc[3], vu[3], vv[3], du[3], dv[3];
+    uint32_t spp, P, C, depth, flags, s_sel, k0, k1;
+    uint32_t row_begin, row_step, col_begin, col_count;
+    uint8_t* rgb;
+    double* lin;
+    unsigned long long* segs;  // kSegShards counters, one per 128-B line
+    uint32_t* err;
+};
+
+constexpr int kSegShards = 256;
+constexpr int kSegStride = 16;  // u64 per shard (128 B)
+
+// Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
+// wave-uniform, so these become s_load into SGPRs — a free broadcast to all 64 lanes.
+template <typename T> using cptr = const __attribute__((address_space(4))) T*;
+
+// Camera::get_ray, ray_tracing.rs:77-89 (jitter stream 0, disk stream 1).
+template <typename T>
+__device__ __forceinline__ void camera_ray(const KParams<T>& p, uint32_t col, uint32_t row, uint32_t pix,
+                                           uint32_t s, V3<T>& o, V3<T>& d) {
+    const U4 r = philox(s, pix, 0u, 0u, p.k0, p.k1);
+    const T xo = u01a(r, T(0)), yo = u01b(r, T(0));
+    const T s1 = ((T)col + xo) / (T)p.W;
+    const T s2 = ((T)row + yo) / (T)p.H;
+    const V3<T> vu = mk(p.vu[0], p.vu[1], p.vu[2]), vv = mk(p.vv[0], p.vv[1], p.vv[2]);
+    const V3<T> pc = add(mk(p.ulc[0], p.ulc[1], p.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
+    T dx = 0, dy = 0;  // random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2
+    for (uint32_t i = 0; i < 256u; ++i) {
+        const U4 q = philox(s, pix, i, 1u, p.k0, p.k1);
+        const T x = T(2.0) * u01a(q, T(0)) - T(1.0);
+        const T y = T(2.0) * u01b(q, T(0)) - T(1.0);
+        if (x * x + y * y <= T(1.0)) { dx = x; dy = y; break; }
+    }
+    const V3<T> orig = add(add(mul(mk(p.du[0], p.du[1], p.du[2]), dx), mul(mk(p.dv[0], p.dv[1], p.dv[2]), dy)),
+                           mk(p.center[0], p.center[1], p.center[2]));
+    o = orig;
+    d = unit(sub(pc, orig));
+}
+
+// One bounce of one enabled ray: the object loop of trace_vectorized2 (ray_tracing.rs:399-403)
+// + the per-lane material step (:406-426).  Returns true if the ray hit (and was scattered).
+template <typename T>
+__device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, V3<T>& col, uint32_t pix,
+                                       uint32_t sid, uint32_t k) {
+    const T a = pk_len2(d);          // objects.rs:253
+    const T inv_a = T(1.0) / a;      // objects.rs:254 (loop-invariant)
+    T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
+    int best = -1;
+    const bool root2 = (p.flags & RT_FLAG_ROOT2) != 0u;
+    cptr<T> sph = (cptr<T>)p.sph;
+    const uint32_t n = p.n_spheres;
+    for (uint32_t i = 0; i < n; ++i) {
+        const T cx = sph[4 * i + 0], cy = sph[4 * i + 1], cz = sph[4 * i + 2], r2 = sph[4 * i + 3];
+        const V3<T> oc = mk(o.x - cx, o.y - cy, o.z - cz);     // :252
+        const T hb = pk_dot(oc, d);                            // :255
+        const T c = pk_len2(oc) - r2;                          // :256
+        const T disc = fma(hb, hb, -a * c);                    // :257
+        if (disc >= T(0.0)) {                                  // :259-261
+            const T sd = sqrt(disc);
+            const T r1 = (-hb - sd) * inv_a;                   // :270
+            bool valid = r1 >= T(0.001) && r1 < T(INFINITY);   // :272
+            T root = r1;
+            if (root2 && !valid) {                             // Q1 off: scalar semantics
+                root = (-hb + sd) * inv_a;                     // :271
+                valid = root >= T(0.001) && root < T(INFINITY);
+            }
+            if (valid && root <= best_t) { best_t = root; best = (int)i; }   // objects.rs:141
+        }
+    }
+    if (best < 0) return false;      // sky: ray_tracing.rs:421-424
+    // PackedHitRecords::finalize (objects.rs:157-162); normal = at_t(t) - center (:279-280)
+    const T* sg = p.sph + 4 * best;
+    const V3<T> cen = mk(sg[0], sg[1], sg[2]);
+    const V3<T> hp = mk(o.x + d.x * best_t, o.y + d.y * best_t, o.z + d.z * best_t);
+    V3<T> nrm = sub(hp, cen);
+    const T len = sqrt(pk_len2(nrm));
+    nrm = mk(nrm.x / len, nrm.y / len, nrm.z / len);
+    const bool front = pk_dot(d, nrm) < T(0.0);
+    if (!front) nrm = neg(nrm);
+    // Material::get_hit_result (materials.rs:54-147); scatter stream 2
+    const MatT<T> m = p.mats[p.smat[best]];
+    const U4 r = philox(sid, pix, k, 2u, p.k0, p.k1);
+    V3<T> nd;
+    if (m.kind == RT_LAMBERTIAN) {
+        nd = add(unit_vec(u01a(r, T(0)), u01b(r, T(0))), nrm);
+        if (near_zero(nd)) nd = nrm;
+        col = mk(col.x * m.ar, col.y * m.ag, col.z * m.ab);
+    } else if (m.kind == RT_METAL) {
+        nd = add(reflect(d, nrm), mul(unit_vec(u01a(r, T(0)), u01b(r, T(0))), m.fuzz));
+        col = mk(col.x * m.ar, col.y * m.ag, col.z * m.ab);
+    } else {
+        const T ratio = front ? T(1.0) / m.ior : m.ior;
+        const V3<T> nn = m.hollow ? neg(nrm) : nrm;
+        const T ct = fmin(dot(neg(d), nn), T(1.0));
+        const T st = sqrt(T(1.0) - ct * ct);
+        bool refl = ratio * st > T(1.0);
+        if (!refl) {   // Dielectric::reflectance (materials.rs:121-124), powi(5) = x*((x*x)*(x*x))
+            const T q = (T(1.0) - ratio) / (T(1.0) + ratio);
+            const T r0 = q * q;
+            const T m1 = T(1.0) - ct;
+            const T m2 = m1 * m1;
+            const T m5 = m1 * (m2 * m2);
+            refl = r0 + (T(1.0) - r0) * m5 > u01a(r, T(0));
+        }
+        nd = refl ? reflect(d, nn) : refract(d, nn, ratio);
+        col = mk(col.x * T(1.0), col.y * T(1.0), col.z * T(1.0));
+    }
+    o = hp;
+    d = nd;
+    return true;
+}
+
+template <typename T> struct Smem {
+    T *ox, *oy, *oz, *dx, *dy, *dz, *cr, *cg, *cb;  // active-ray state by position
+    T *vr, *vg, *vb;                                 // retired value by position
+    T* yv;                                           // primary-ray y by position (Q2)
+    uint32_t* sid;                                   // sample id by position (RNG key)
+    uint32_t* wcnt;                                  // survivors per (slot, wave) group
+    T* part;                                         // 12 partial sums
+};
+
+__host__ __device__ inline size_t smem_bytes(uint32_t P, size_t tsz) {
+    return (size_t)P * (13 * tsz + 4) + 64 * 4 + 16 * tsz;
+}
+
+template <typename T>
+__device__ __forceinline__ Smem<T> carve(char* base, uint32_t P) {
+    Smem<T> s;
+    T* t = (T*)base;
+    s.ox = t; t += P; s.oy = t; t += P; s.oz = t; t += P;
+    s.dx = t; t += P; s.dy = t; t += P; s.dz = t; t += P;
+    s.cr = t; t += P; s.cg = t; t += P; s.cb = t; t += P;
+    s.vr = t; t += P; s.vg = t; t += P; s.vb = t; t += P;
+    s.yv = t; t += P;
+    s.part = t; t += 16;
+    uint32_t* u = (uint32_t*)t;
+    s.sid = u; u += P;
+    s.wcnt = u;
+    return s;
+}
+
+template <typename T, int S>
+__global__ __launch_bounds__(1024) void trace_pixels(KParams<T> p) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const uint32_t NT = blockDim.x;
+    const uint32_t NW = NT >> 6;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
+    const uint32_t P = p.P, spp = p.spp, depth = p.depth;
+    Smem<T> sm = carve<T>(smem_raw, P);
+
+    const uint32_t b = blockIdx.x;
+    const uint32_t ri = b / p.col_count, ci = b % p.col_count;
+    const uint32_t row = p.row_begin + ri * p.row_step, col = p.col_begin + ci;
+    const uint32_t pix = row * p.W + col;
+
+    // Retired-value array init.  Positions [spp, P) are the missing lanes of a partial last
+    // chunk: disabled from the start (ray.rs:140-144), hit_sky at bounce 0 (:421-424), zero
+    // primary direction -> sky(0); with depth 0 they keep white in buffer 0 (s_sel==0).
+    {
+        const V3<T> s0 = sky(T(0.0));
+        for (uint32_t q = tid; q < P; q += NT) {
+            T vr = 0, vg = 0, vb = 0;
+            if (q >= spp) {
+                if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
+                else if (p.s_sel == 0u) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
+            }
+            sm.vr[q] = vr; sm.vg[q] = vg; sm.vb[q] = vb;
+        }
+    }
+
+    V3<T> ro[S], rd[S], rc[S];
+    uint32_t rs[S];
+    uint32_t n = spp;            // active rays, at positions [0, n)
+    uint32_t Lcur = p.C;         // last_active_chunk (ray_tracing.rs:386)
+    uint64_t nseg = 0;
+    for (uint32_t k = 0; k < depth; ++k) {
+        bool act[S], surv[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            const uint32_t pos = (uint32_t)j * NT + tid;
+            act[j] = pos < n;
+            surv[j] = false;
+            if (act[j]) {
+                if (k == 0) {
+                    camera_ray(p, col, row, pix, pos, ro[j], rd[j]);
+                    rc[j] = mk(T(1.0), T(1.0), T(1.0));
+                    rs[j] = pos;
+                    sm.yv[pos] = rd[j].y;
+                } else {
+                    ro[j] = mk(sm.ox[pos], sm.oy[pos], sm.oz[pos]);
+                    rd[j] = mk(sm.dx[pos], sm.dy[pos], sm.dz[pos]);
+                    rc[j] = mk(sm.cr[pos], sm.cg[pos], sm.cb[pos]);
+                    rs[j] = sm.sid[pos];
+                }
+                surv[j] = bounce(p, ro[j], rd[j], rc[j], pix, rs[j], k);
+            }
+        }
+        nseg += n;
+        unsigned long long bal[S];
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            bal[j] = __ballot(act[j] && surv[j]);
+            if (lane == 0) sm.wcnt[j * NW + wave] = (uint32_t)__popcll(bal[j]);
+        }
+        __syncthreads();
+        uint32_t n_next = 0;
+        const uint32_t ng = (uint32_t)S * NW;
+        for (uint32_t g = 0; g < ng; ++g) n_next += sm.wcnt[g];
+        const uint32_t Lnext = (k + 1 == depth) ? 0u : (n_next + 3u) / 4u;
+        const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;
+        const bool U = p.s_sel == (k & 1u);   // final read hits this bounce's unsorted buffer
+#pragma unroll
+        for (int j = 0; j < S; ++j) {
+            if (!act[j]) continue;
+            const uint32_t pos = (uint32_t)j * NT + tid;
+            const uint32_t g = (uint32_t)j * NW + wave;
+            uint32_t base = 0;
+            for (uint32_t h = 0; h < g; ++h) base += sm.wcnt[h];
+            const uint32_t below = (uint32_t)__popcll(bal[j] & ((1ull << lane) - 1ull));
+            const uint32_t rank = base + below;   // survivors before `pos`
+            if (surv[j]) {
+                sm.ox[rank] = ro[j].x; sm.oy[rank] = ro[j].y; sm.oz[rank] = ro[j].z;
+                sm.dx[rank] = rd[j].x; sm.dy[rank] = rd[j].y; sm.dz[rank] = rd[j].z;
+                sm.cr[rank] = rc[j].x; sm.cg[rank] = rc[j].y; sm.cb[rank] = rc[j].z;
+                sm.sid[rank] = rs[j];
+            } else {
+                const uint32_t pnew = n_next + (pos - rank);
+                const bool old_in = pos >= lo && pos < hi;
+                const bool new_in = pnew >= lo && pnew < hi;
+                if (U && old_in) {
+                    const V3<T> s = sky(sm.yv[pos]);
+                    sm.vr[pos] = rc[j].x * s.x; sm.vg[pos] = rc[j].y * s.y; sm.vb[pos] = rc[j].z * s.z;
+                }
+                if (!U || !new_in) {
+                    const V3<T> s = sky(sm.yv[pnew]);
+                    sm.vr[pnew] = rc[j].x * s.x; sm.vg[pnew] = rc[j].y * s.y; sm.vb[pnew] = rc[j].z * s.z;
+                }
+            }
+        }
+        __syncthreads();
+        n = n_next;
+        Lcur = Lnext;
+        if (n == 0) break;
+    }
+
+    // Final reduction in the reference's order: per lane l, sum chunks j = 0..C-1 from +0.0
+    // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
+    if (tid < 12) {
+        const uint32_t ch = tid >> 2, l = tid & 3u;
+        const T* v = ch == 0 ? sm.vr : (ch == 1 ? sm.vg : sm.vb);
+        T acc = T(0.0);
+        for (uint32_t j = 0; j < p.C; ++j) acc = acc + v[4 * j + l];
+        sm.part[tid] = acc;
+    }
+    __syncthreads();
+    if (tid < 3) {
+        const T* s4 = sm.part + 4 * tid;
+        const T tot = (((T(0.0) + s4[0]) + s4[1]) + s4[2]) + s4[3];
+        const T v = tot / (T)spp;                                   // renderer.rs:161
+        if (!(v <= T(2.0))) atomicOr(p.err, 1u);                    // color.rs:55-57 assert
+        if (p.rgb) p.rgb[(size_t)b * 3 + tid] = q8(v);
+        if (p.lin) p.lin[(size_t)b * 3 + tid] = (double)v;
+    }
+    if (tid == 0) atomicAdd(&p.segs[(b & (kSegShards - 1)) * kSegStride], (unsigned long long)nseg);
+}
+
+}  // namespace rt
+
+// ============================== host side ==============================
+using namespace rt;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(x)                                                                     \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) return fail(RT_ERR_HIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct rt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev_first = nullptr, ev_last = nullptr;
+    bool have_first = false;
+    // scene, fp64 and fp32 images
+    void* sph64 = nullptr; void* sph32 = nullptr;
+    void* mat64 = nullptr; void* mat32 = nullptr;
+    uint32_t* smat = nullptr;
+    uint32_t n_spheres = 0, n_materials = 0;
+    unsigned long long* segs = nullptr;
+    uint32_t* err = nullptr;
+    uint64_t samples = 0, pixels = 0;
+};
+
+extern "C" const char* rt_last_error(void) { return g_err.c_str(); }
+extern "C" const char* rt_version(void) { return "rt_mi355x 0.1 gfx950"; }
+
+extern "C" double rt_metal_clamp_fuzz(double fuzz) { return fuzz < 1.0 ? fuzz : 1.0; }
+
+// Camera::new, ray_tracing.rs:27-62 (f64, Vec3 ops without FMA; compiled -ffp-contract=off).
+extern "C" int rt_camera_new(rt_camera* out, uint32_t w, uint32_t h, double focal_length, double view_angle_deg,
+                             const double center[3], const double look_at[3], const double up[3],
+                             double defocus_angle_deg) {
+    if (!out || !center || !look_at || !up || w == 0 || h == 0) return fail(RT_ERR_INVALID, "rt_camera_new: bad argument");
+    const double rads_per_deg = 3.141592653589793 / 180.0;              // f64::to_radians
+    const double aspect = (double)w / (double)h;                         // :28
+    const double vh = std::tan((view_angle_deg * rads_per_deg) / 2.0) * focal_length * 2.0;  // :29
+    const double vw = vh * aspect;                                       // :32
+    auto unit3 = [](const double a[3], double o[3]) {
+        const double l = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        o[0] = a[0] / l; o[1] = a[1] / l; o[2] = a[2] / l;
+    };
+    double dirv[3] = {look_at[0] - center[0], look_at[1] - center[1], look_at[2] - center[2]};
+    double dir[3]; unit3(dirv, dir);                                     // :34
+    const double wv[3] = {-dir[0], -dir[1], -dir[2]};                    // :35
+    const double cr[3] = {up[1] * wv[2] - up[2] * wv[1], up[2] * wv[0] - up[0] * wv[2], up[0] * wv[1] - up[1] * wv[0]};
+    double u[3]; unit3(cr, u);                                           // :36
+    const double v[3] = {wv[1] * u[2] - wv[2] * u[1], wv[2] * u[0] - wv[0] * u[2], wv[0] * u[1] - wv[1] * u[0]};  // :37
+    const double dr = focal_length * std::tan((defocus_angle_deg / 2.0) * rads_per_deg);  // :43
+    out->image_width = w; out->image_height = h;
+    for (int i = 0; i < 3; ++i) {
+        out->center[i] = center[i];
+        out->vu[i] = u[i] * vw;                                          // :39
+        out->vv[i] = (-v[i]) * vh;                                       // :40
+        out->ulc[i] = ((center[i] - wv[i] * focal_length) - out->vu[i] / 2.0) - out->vv[i] / 2.0;  // :41
+        out->du[i] = u[i] * dr;                                          // :44
+        out->dv[i] = v[i] * dr;                                          // :45
+    }
+    return RT_OK;
+}
+
+extern "C" int rt_context_create(int device, rt_context** out) {
+    if (!out) return fail(RT_ERR_INVALID, "rt_context_create: out is NULL");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID, "rt_context_create: no such device");
+    HIPCHK(hipSetDevice(device));
+    rt_context* c = new rt_context();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&c->ev_first));
+    HIPCHK(hipEventCreate(&c->ev_last));
+    HIPCHK(hipMalloc((void**)&c->segs, sizeof(unsigned long long) * kSegShards * kSegStride));
+    HIPCHK(hipMalloc((void**)&c->err, 16));
+    HIPCHK(hipMemset(c->segs, 0, sizeof(unsigned long long) * kSegShards * kSegStride));
+    HIPCHK(hipMemset(c->err, 0, 16));
+    *out = c;
+    return RT_OK;
+}
+
+static void free_scene(rt_context* c) {
+    (void)hipFree(c->sph64); (void)hipFree(c->sph32); (void)hipFree(c->mat64); (void)hipFree(c->mat32);
+    (void)hipFree(c->smat);
+    c->sph64 = c->sph32 = c->mat64 = c->mat32 = nullptr;
+    c->smat = nullptr;
+    c->n_spheres = c->n_materials = 0;
+}
+
+extern "C" int rt_context_destroy(rt_context* c) {
+    if (!c) return RT_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    (void)hipFree(c->segs); (void)hipFree(c->err);
+    (void)hipEventDestroy(c->ev_first); (void)hipEventDestroy(c->ev_last);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return RT_OK;
+}
+
+template <typename T>
+static void pack_scene(const rt_scene* s, std::vector<T>& sph, std::vector<MatT<T>>& mats) {
+    sph.resize((size_t)4 * (s->n_spheres ? s->n_spheres : 1));
+    for (uint32_t i = 0; i < s->n_spheres; ++i) {
+        const T r = (T)s->radius[i];
+        sph[4 * i + 0] = (T)s->center[3 * i + 0];
+        sph[4 * i + 1] = (T)s->center[3 * i + 1];
+        sph[4 * i + 2] = (T)s->center[3 * i + 2];
+        sph[4 * i + 3] = r * r;   // self.radius.powi(2) in T (objects.rs:256)
+    }
+    mats.resize(s->n_materials ? s->n_materials : 1);
+    for (uint32_t i = 0; i < s->n_materials; ++i) {
+        const rt_material& m = s->materials[i];
+        mats[i] = MatT<T>{m.kind, m.hollow, (T)m.albedo[0], (T)m.albedo[1], (T)m.albedo[2], (T)m.fuzz, (T)m.ior};
+    }
+}
+
+extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
+    if (!c || !s) return fail(RT_ERR_INVALID, "rt_context_set_scene: NULL argument");
+    if (s->n_spheres && (!s->center || !s->radius || !s->material || !s->materials))
+        return fail(RT_ERR_INVALID, "rt_context_set_scene: NULL array");
+    for (uint32_t i = 0; i < s->n_spheres; ++i)
+        if (s->material[i] >= s->n_materials)
+            return fail(RT_ERR_INVALID, "rt_context_set_scene: material index out of range (objects.rs:296 would panic)");
+    for (uint32_t i = 0; i < s->n_materials; ++i)
+        if (s->materials[i].kind > RT_DIELECTRIC)
+            return fail(RT_ERR_INVALID, "rt_context_set_scene: unknown material kind (materials.rs:31 would panic)");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    free_scene(c);
+    std::vector<double> s64; std::vector<MatT<double>> m64;
+    std::vector<float> s32; std::vector<MatT<float>> m32;
+    pack_scene(s, s64, m64);
+    pack_scene(s, s32, m32);
+    std::vector<uint32_t> sm(s->n_spheres ? s->n_spheres : 1, 0);
+    for (uint32_t i = 0; i < s->n_spheres; ++i) sm[i] = s->material[i];
+    HIPCHK(hipMalloc(&c->sph64, s64.size() * sizeof(double)));
+    HIPCHK(hipMalloc(&c->sph32, s32.size() * sizeof(float)));
+    HIPCHK(hipMalloc(&c->mat64, m64.size() * sizeof(MatT<double>)));
+    HIPCHK(hipMalloc(&c->mat32, m32.size() * sizeof(MatT<float>)));
+    HIPCHK(hipMalloc((void**)&c->smat, sm.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->sph64, s64.data(), s64.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->sph32, s32.data(), s32.size() * sizeof(float), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->mat64, m64.data(), m64.size() * sizeof(MatT<double>), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->mat32, m32.data(), m32.size() * sizeof(MatT<float>), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->smat, sm.data(), sm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->n_spheres = s->n_spheres;
+    c->n_materials = s->n_materials;
+    return RT_OK;
+}
+
+static bool check_range(const rt_camera* cam, const rt_tile_range* r) {
+    if (r->row_count == 0 || r->col_count == 0 || r->row_step == 0) return false;
+    if (r->col_begin + (uint64_t)r->col_count > cam->image_width) return false;
+    const uint64_t last_row = r->row_begin + (uint64_t)(r->row_count - 1) * r->row_step;
+    return last_row < cam->image_height;
+}
+
+template <typename T, int S>
+static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_t spp, uint64_t seed, uint32_t flags,
+                    const rt_tile_range& rg, void* d_rgb, void* d_lin, hipStream_t st, uint32_t NT, size_t lds) {
+    KParams<T> p;
+    memset(&p, 0, sizeof(p));
+    const bool f64 = sizeof(T) == 8;
+    p.sph = (const T*)(f64 ? c->sph64 : c->sph32);
+    p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
+    p.smat = c->smat;
+    p.n_spheres = c->n_spheres;
+    p.W = cam->image_width; p.H = cam->image_height;
+    for (int i = 0; i < 3; ++i) {
+        p.center[i] = (T)cam->center[i]; p.ulc[i] = (T)cam->ulc[i]; p.vu[i] = (T)cam->vu[i];
+        p.vv[i] = (T)cam->vv[i]; p.du[i] = (T)cam->du[i]; p.dv[i] = (T)cam->dv[i];
+    }
+    p.spp = spp;
+    p.C = (spp + 3) / 4;
+    p.P = 4 * p.C;
+    p.depth = depth;
+    p.flags = flags;
+    p.s_sel = (p.C - 1) % 2;   // ray_tracing.rs:486
+    p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32);
+    p.row_begin = rg.row_begin; p.row_step = rg.row_step; p.col_begin = rg.col_begin; p.col_count = rg.col_count;
+    p.rgb = (uint8_t*)d_rgb;
+    p.lin = (double*)d_lin;
+    p.segs = c->segs;
+    p.err = c->err;
+    auto kern = trace_pixels<T, S>;
+    HIPCHK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    const uint64_t nblocks = (uint64_t)rg.row_count * rg.col_count;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3(NT), lds, st, p);
+    HIPCHK(hipGetLastError());
+    return RT_OK;
+}
+
+extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max_bounces, uint32_t spp, uint64_t seed,
+                               uint32_t flags, const rt_tile_range* range, void* d_rgb8, void* d_linear, void* stream) {
+    if (!c || !cam) return fail(RT_ERR_INVALID, "rt_render_async: NULL argument");
+    if (spp == 0) return fail(RT_ERR_INVALID, "rt_render_async: spp == 0 (the reference panics: 0/0 in to_u8_array)");
+    if (cam->image_width == 0 || cam->image_height == 0) return fail(RT_ERR_INVALID, "rt_render_async: empty image");
+    if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "image too large");
+    rt_tile_range rg = range ? *range : rt_tile_range{0, 1, cam->image_height, 0, cam->image_width};
+    if (!check_range(cam, &rg)) return fail(RT_ERR_INVALID, "rt_render_async: tile range outside the image");
+    if ((uint64_t)rg.row_count * rg.col_count > 0x7FFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "too many pixels in one call");
+    const uint32_t C = (spp + 3) / 4, P = 4 * C;
+    uint32_t NT = P < 1024 ? ((P + 63) / 64) * 64 : 1024;
+    const uint32_t S = (P + NT - 1) / NT;
+    const bool f32 = (flags & RT_FLAG_F32) != 0;
+    const size_t lds = smem_bytes(P, f32 ? 4 : 8);
+    if (S > 2 || lds > 160 * 1024)
+        return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp too large for the per-pixel LDS budget in this precision");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if (!c->have_first) {
+        HIPCHK(hipEventRecord(c->ev_first, st));
+        c->have_first = true;
+    }
+    int rc;
+    if (f32) rc = S == 1 ? launch_t<float, 1>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds)
+                         : launch_t<float, 2>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds);
+    else rc = S == 1 ? launch_t<double, 1>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds)
+                     : launch_t<double, 2>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds);
+    if (rc != RT_OK) return rc;
+    HIPCHK(hipEventRecord(c->ev_last, st));
+    c->pixels += (uint64_t)rg.row_count * rg.col_count;
+    c->samples += (uint64_t)rg.row_count * rg.col_count * spp;
+    return RT_OK;
+}
+
+extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
+    if (!c) return fail(RT_ERR_INVALID, "rt_context_collect: NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<unsigned long long> segs(kSegShards * kSegStride);
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(segs.data(), c->segs, segs.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&err, c->err, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    float ms = 0.f;
+    if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
+    HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(c->err, 0, 16));
+    uint64_t total = 0;
+    for (int i = 0; i < kSegShards; ++i) total += segs[(size_t)i * kSegStride];
+    if (out) {
+        memset(out, 0, sizeof(*out));
+        out->kernel_ms = ms;
+        out->pixels = c->pixels;
+        out->samples = c->samples;
+        out->ray_segments = total;
+    }
+    c->have_first = false;
+    c->pixels = c->samples = 0;
+    if (err) return fail(RT_ERR_RANGE, "a pixel channel exceeded 2.0 (Color::to_u8_array would panic, color.rs:55-57)");
+    return RT_OK;
+}
+
+extern "C" int rt_device_alloc(rt_context* c, size_t bytes, void** out) {
+    if (!c || !out) return fail(RT_ERR_INVALID, "rt_device_alloc: NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(out, bytes ? bytes : 1));
+    return RT_OK;
+}
+extern "C" int rt_device_free(rt_context* c, void* ptr) {
+    if (!c) return fail(RT_ERR_INVALID, "rt_device_free: NULL context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipFree(ptr));
+    return RT_OK;
+}
+extern "C" int rt_memcpy_d2h(rt_context* c, void* dst, const void* src, size_t bytes) {
+    if (!c || !dst || !src) return fail(RT_ERR_INVALID, "rt_memcpy_d2h: NULL argument");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return RT_OK;
+}
+
+extern "C" int rt_render(const rt_scene* scene, const rt_camera* cam, uint32_t max_bounces, uint32_t spp, uint64_t seed,
+                         uint32_t flags, const rt_tile_range* range, uint8_t* rgb8, double* linear, rt_stats* stats) {
+    if (!scene || !cam) return fail(RT_ERR_INVALID, "rt_render: NULL argument");
+    const auto t0 = std::chrono::steady_clock::now();
+    rt_context* c = nullptr;
+    int rc = rt_context_create(0, &c);
+    if (rc != RT_OK) return rc;
+    struct Guard { rt_context* c; void* a = nullptr; void* b = nullptr;
+        ~Guard() { if (a) rt_device_free(c, a); if (b) rt_device_free(c, b); rt_context_destroy(c); } } g{c};
+    rc = rt_context_set_scene(c, scene);
+    if (rc != RT_OK) return rc;
+    const rt_tile_range rg = range ? *range : rt_tile_range{0, 1, cam->image_height, 0, cam->image_width};
+    const size_t npx = (size_t)rg.row_count * rg.col_count;
+    if (rgb8 && (rc = rt_device_alloc(c, npx * 3, &g.a)) != RT_OK) return rc;
+    if (linear && (rc = rt_device_alloc(c, npx * 3 * sizeof(double), &g.b)) != RT_OK) return rc;
+    rc = rt_render_async(c, cam, max_bounces, spp, seed, flags, &rg, g.a, g.b, nullptr);
+    if (rc != RT_OK) return rc;
+    rt_stats st;
+    const int crc = rt_context_collect(c, nullptr, &st);
+    if (crc != RT_OK && crc != RT_ERR_RANGE) return crc;
+    if (rgb8 && (rc = rt_memcpy_d2h(c, rgb8, g.a, npx * 3)) != RT_OK) return rc;
+    if (linear && (rc = rt_memcpy_d2h(c, linear, g.b, npx * 3 * sizeof(double))) != RT_OK) return rc;
+    st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    st.pixels_per_second = st.seconds > 0 ? (double)st.pixels / st.seconds : 0.0;
+    if (stats) *stats = st;
+    if (crc == RT_ERR_RANGE) return fail(RT_ERR_RANGE, "a pixel channel exceeded 2.0 (Color::to_u8_array would panic, color.rs:55-57)");
+    return RT_OK;
+}

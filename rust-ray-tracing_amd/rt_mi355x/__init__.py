@@ -1,0 +1,15 @@
+"""rt_mi355x — MI355X-native drop-in for rust-ray-tracing's per-pixel sample loop.
+
+Python view of the C ABI in include/rt_mi355x.h (the product is the HIP library
+lib/librt_mi355x.so; this package only binds it and mirrors the reference's host types).
+"""
+from . import abi
+from .abi import load_library, RtError
+from .scene import Camera, Dielectric, FlatScene, Lambertian, Metal, Scene, Sphere, MAIN_CAMERA, camera_new_py
+from .renderer import GpuRenderer, RenderStat, Renderer
+from . import scenes
+
+__all__ = [
+    "abi", "load_library", "RtError", "Camera", "Dielectric", "FlatScene", "Lambertian", "Metal", "Scene",
+    "Sphere", "MAIN_CAMERA", "camera_new_py", "GpuRenderer", "RenderStat", "Renderer", "scenes",
+]

@@ -1,0 +1,172 @@
+"""GPU parity: the HIP megakernel (through the C ABI) against the CPU restatement in oracle/.
+
+Bar: same (seed, pixel, sample) keys -> the kernel follows the oracle's exact arithmetic
+(FMA placement, correctly rounded div/sqrt, reference summation order), so the per-pixel
+linear colours must be BIT-IDENTICAL in both fp64 and fp32 mode, and RGB8 byte-identical.
+Tolerance stated for the record: 0 ulp (we assert array_equal).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import rt_mi355x as rt
+from rt_mi355x import abi
+from oracle_bind import oracle_render
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0001
+
+
+def cam_for(w, h):
+    return rt.camera_new_py(w, h, **rt.MAIN_CAMERA)
+
+
+def gpu(renderer, flat, cam, depth, spp, seed=SEED, flags=0, tile=None):
+    renderer.seed = seed
+    renderer.flags = flags
+    rgb, lin, st, rc = renderer.render_flat(depth, spp, flat, cam, tile_range=tile, want_linear=True)
+    return rgb, lin, st, rc
+
+
+def assert_parity(renderer, flat, cam, depth, spp, flags=0, seed=SEED):
+    prec = "f32" if flags & abi.RT_FLAG_F32 else "f64"
+    rgb_g, lin_g, st, rc_g = gpu(renderer, flat, cam, depth, spp, seed, flags)
+    rgb_o, lin_o, segs_o, rc_o = oracle_render(flat, cam, depth, spp, seed, flags & abi.RT_FLAG_ROOT2,
+                                               precision=prec)
+    assert rc_g == rc_o
+    diff = np.argwhere(lin_g != lin_o)
+    assert diff.size == 0, (
+        f"{len(diff)} mismatching channels; first pixel {diff[0][0]}: gpu {lin_g[diff[0][0]]} oracle {lin_o[diff[0][0]]}")
+    np.testing.assert_array_equal(rgb_g, rgb_o)
+    assert st.ray_segments == segs_o
+    assert st.samples == cam.image_width * cam.image_height * spp
+    return lin_g, st
+
+
+@pytest.fixture(scope="module")
+def scene_a():
+    return rt.scenes.config_scene("A").flatten()
+
+
+@pytest.fixture(scope="module")
+def scene_100():
+    return rt.scenes.random_spheres(100).flatten()
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_config_a_full(renderer, scene_a, flags):
+    """Config A exactly as BASELINE.json names it: 400x225, 3 spheres, 16 spp, 8 bounces."""
+    lin, st = assert_parity(renderer, scene_a, cam_for(400, 225), 8, 16, flags)
+    assert 0.0 < lin.mean() < 1.0
+
+
+@pytest.mark.parametrize("spp", [1, 4, 6, 32, 100])
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_random_scene_spp(renderer, scene_100, spp, flags):
+    """spp 1/6 exercise partial chunks, 100 has (C-1)%2 == 0 (quirk Q3's other buffer)."""
+    assert_parity(renderer, scene_100, cam_for(96, 54), 50, spp, flags)
+
+
+@pytest.mark.parametrize("depth", [0, 1, 2, 3])
+@pytest.mark.parametrize("spp", [6, 8, 12])
+def test_depth_edges(renderer, scene_100, depth, spp):
+    assert_parity(renderer, scene_100, cam_for(48, 27), depth, spp, 0)
+
+
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_ROOT2, abi.RT_FLAG_ROOT2 | abi.RT_FLAG_F32])
+def test_root2_mode(renderer, scene_100, flags):
+    assert_parity(renderer, scene_100, cam_for(64, 36), 50, 16, flags)
+
+
+def test_empty_scene(renderer):
+    """hitables = [] -> every sample misses at bounce 0: pixel = mean sky(primary y)."""
+    flat = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((0.5, 0.5, 0.5))])
+    lin, st = assert_parity(renderer, flat, cam_for(40, 30), 8, 8, 0)
+    assert np.all((lin > 0.5) & (lin <= 1.0)) and st.ray_segments == 40 * 30 * 8
+
+
+def test_large_spp(renderer, scene_100):
+    assert_parity(renderer, scene_100, cam_for(8, 6), 50, 1024, 0)            # P = 1024, fp64
+    assert_parity(renderer, scene_100, cam_for(8, 6), 50, 2048, abi.RT_FLAG_F32)  # two slots per thread
+
+
+def test_fp64_2048_unsupported(renderer, scene_100):
+    with pytest.raises(rt.RtError) as e:
+        gpu(renderer, scene_100, cam_for(8, 6), 50, 2048, flags=0)
+    assert e.value.code == abi.RT_ERR_UNSUPPORTED
+
+
+def test_tile_ranges_compose(renderer, scene_100):
+    """Row-interleaved shards (the multi-GPU partition) reassemble the full image bit-exactly."""
+    cam = cam_for(64, 36)
+    _, full, _, _ = gpu(renderer, scene_100, cam, 50, 16)
+    full = full.reshape(36, 64, 3)
+    for world in (2, 3):
+        for r in range(world):
+            rows = len(range(r, 36, world))
+            tile = abi.RtTileRange(r, world, rows, 0, 64)
+            _, part, _, _ = gpu(renderer, scene_100, cam, 50, 16, tile=tile)
+            np.testing.assert_array_equal(part.reshape(rows, 64, 3), full[r::world])
+    tile = abi.RtTileRange(5, 1, 7, 11, 20)
+    _, part, _, _ = gpu(renderer, scene_100, cam, 50, 16, tile=tile)
+    np.testing.assert_array_equal(part.reshape(7, 20, 3), full[5:12, 11:31])
+
+
+def test_range_error(renderer):
+    """albedo > 1 pushes a pixel above 2.0: the reference panics (color.rs:55-57); we return
+    RT_ERR_RANGE with the image written, and the oracle flags the same pixels."""
+    flat = rt.FlatScene(np.array([[0.0, 0.0, 0.0]]), np.array([5.0]), np.array([0], np.uint32),
+                        [rt.Lambertian((9.0, 9.0, 9.0))])
+    cam = cam_for(16, 9)
+    rgb_g, lin_g, _, rc = gpu(renderer, flat, cam, 4, 8)
+    rgb_o, lin_o, _, rc_o = oracle_render(flat, cam, 4, 8, SEED)
+    assert rc == abi.RT_ERR_RANGE and rc_o == abi.RT_ERR_RANGE
+    np.testing.assert_array_equal(lin_g, lin_o)
+    np.testing.assert_array_equal(rgb_g, rgb_o)
+
+
+def test_invalid_arguments(renderer, scene_100, lib):
+    cam = cam_for(8, 6)
+    with pytest.raises(rt.RtError) as e:
+        gpu(renderer, scene_100, cam, 8, 0)
+    assert e.value.code == abi.RT_ERR_INVALID
+    bad = rt.FlatScene(np.zeros((1, 3)), np.ones(1), np.array([3], np.uint32), [rt.Lambertian((1, 1, 1))])
+    rc = lib.rt_context_set_scene(renderer.ctx, ctypes.byref(bad.abi))
+    assert rc == abi.RT_ERR_INVALID
+    assert b"material index" in lib.rt_last_error()
+    with pytest.raises(rt.RtError):
+        gpu(renderer, scene_100, cam, 8, 4, tile=abi.RtTileRange(0, 1, 7, 0, 8))   # 7 rows > 6
+
+
+def test_one_shot_rt_render(lib, scene_100):
+    """rt_render (host in/out) equals the device-resident path."""
+    cam = cam_for(32, 18)
+    rgb = np.zeros((32 * 18, 3), np.uint8)
+    lin = np.zeros((32 * 18, 3), np.float64)
+    st = abi.RtStats()
+    rc = lib.rt_render(ctypes.byref(scene_100.abi), ctypes.byref(cam), 50, 16, SEED, 0, None,
+                       rgb.ctypes.data, lin.ctypes.data, ctypes.byref(st))
+    assert rc == abi.RT_OK
+    rgb_o, lin_o, segs, _ = oracle_render(scene_100, cam, 50, 16, SEED)
+    np.testing.assert_array_equal(lin, lin_o)
+    assert st.ray_segments == segs and st.seconds > 0
+
+
+def test_seed_changes_image(renderer, scene_100):
+    cam = cam_for(32, 18)
+    _, a, _, _ = gpu(renderer, scene_100, cam, 50, 8, seed=1)
+    _, b, _, _ = gpu(renderer, scene_100, cam, 50, 8, seed=2)
+    _, c, _, _ = gpu(renderer, scene_100, cam, 50, 8, seed=1)
+    assert not np.array_equal(a, b)
+    np.testing.assert_array_equal(a, c)
+
+
+def test_renderer_trait(renderer):
+    """GpuRenderer.render mirrors Renderer::render (renderer.rs:38-40)."""
+    scene = rt.scenes.three_spheres()
+    cam = rt.Camera(40, 30, **rt.MAIN_CAMERA)
+    img, stat = renderer.render(8, 16, scene, cam)
+    assert img.shape == (30, 40, 3) and img.dtype == np.uint8
+    assert stat.pixels_rendered() == 1200 and stat.pixels_per_second() > 0
