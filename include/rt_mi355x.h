@@ -84,6 +84,9 @@ typedef struct rt_stats {
     uint64_t pixels;
     uint64_t samples;        /* pixels * spp */
     uint64_t ray_segments;   /* enabled rays traced, summed over bounces (ray_tracing.rs:396-401) */
+    uint64_t lane_slots;     /* SIMD lanes issued for those traces (64 per wave-bounce);
+                                ray_segments / lane_slots = lane utilisation */
+    uint64_t bounce_iters;   /* bounce-loop iterations executed, summed over pixels */
 } rt_stats;
 
 /* ---- flags ---- */

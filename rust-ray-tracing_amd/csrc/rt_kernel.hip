@@ -42,6 +42,20 @@ template <typename T> struct MatT {
     T ar, ag, ab, fuzz, ior;
 };
 
+template <typename T> struct alignas(4 * sizeof(T)) SphT { T cx, cy, cz, r2; };
+template <typename T> struct alignas(64) SphGroup { SphT<T> s[64 / sizeof(SphT<T>)]; };
+
+// One 64-byte scalar load worth of spheres (s_load_dwordx16 into SGPRs).
+template <typename T>
+__device__ __forceinline__ SphGroup<T> load_group(const __attribute__((address_space(4))) T* f, uint32_t g) {
+    constexpr int NE = 64 / sizeof(T);
+    SphGroup<T> r;
+    T* out = &r.s[0].cx;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) out[e] = f[g * NE + e];
+    return r;
+}
+
 template <typename T> struct KParams {
     const T* sph;              // [n][4] = cx, cy, cz, r*r (r.powi(2), objects.rs:256) in T
     const uint32_t* smat;      // [n] material index
@@ -97,25 +111,43 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
     int best = -1;
     const bool root2 = (p.flags & RT_FLAG_ROOT2) != 0u;
-    cptr<T> sph = (cptr<T>)p.sph;
     const uint32_t n = p.n_spheres;
-    for (uint32_t i = 0; i < n; ++i) {
-        const T cx = sph[4 * i + 0], cy = sph[4 * i + 1], cz = sph[4 * i + 2], r2 = sph[4 * i + 3];
-        const V3<T> oc = mk(o.x - cx, o.y - cy, o.z - cz);     // :252
-        const T hb = pk_dot(oc, d);                            // :255
-        const T c = pk_len2(oc) - r2;                          // :256
-        const T disc = fma(hb, hb, -a * c);                    // :257
-        if (disc >= T(0.0)) {                                  // :259-261
+    // Sphere::hit_packed (objects.rs:249-290) + PackedHitRecords::update (objects.rs:140-155)
+    auto test = [&](const SphT<T>& s, uint32_t i) {
+        const V3<T> oc = mk(o.x - s.cx, o.y - s.cy, o.z - s.cz);   // :252
+        const T hb = pk_dot(oc, d);                                // :255
+        const T c = pk_len2(oc) - s.r2;                            // :256
+        const T disc = fma(hb, hb, -a * c);                        // :257
+        if (disc >= T(0.0)) {                                      // :259-261
             const T sd = sqrt(disc);
-            const T r1 = (-hb - sd) * inv_a;                   // :270
-            bool valid = r1 >= T(0.001) && r1 < T(INFINITY);   // :272
+            const T r1 = (-hb - sd) * inv_a;                       // :270
+            bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
             T root = r1;
-            if (root2 && !valid) {                             // Q1 off: scalar semantics
-                root = (-hb + sd) * inv_a;                     // :271
+            if (root2 && !valid) {                                 // Q1 off: scalar semantics
+                root = (-hb + sd) * inv_a;                         // :271
                 valid = root >= T(0.001) && root < T(INFINITY);
             }
-            if (valid && root <= best_t) { best_t = root; best = (int)i; }   // objects.rs:141
+            if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
         }
+    };
+    // Spheres stream through the scalar cache in 64-byte groups (4 x f32 or 2 x f64 spheres =
+    // one s_load_dwordx16); group g+1 is requested before group g is tested so the K$ latency
+    // hides behind G*13 VALU ops.
+    constexpr uint32_t G = 64 / sizeof(SphT<T>);
+    cptr<T> f = (cptr<T>)__builtin_assume_aligned(p.sph, 64);
+    const uint32_t ng = n / G;
+    if (ng > 0) {
+        SphGroup<T> cur = load_group(f, 0);
+        for (uint32_t g = 0; g < ng; ++g) {
+            const SphGroup<T> nxt = load_group(f, g + 1 < ng ? g + 1 : g);
+#pragma unroll
+            for (uint32_t j = 0; j < G; ++j) test(cur.s[j], g * G + j);
+            cur = nxt;
+        }
+    }
+    for (uint32_t i = ng * G; i < n; ++i) {
+        const SphT<T> s{f[4 * i + 0], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]};
+        test(s, i);
     }
     if (best < 0) return false;      // sky: ray_tracing.rs:421-424
     // PackedHitRecords::finalize (objects.rs:157-162); normal = at_t(t) - center (:279-280)
@@ -222,7 +254,7 @@ __global__ __launch_bounds__(1024) void trace_pixels(KParams<T> p) {
     uint32_t rs[S];
     uint32_t n = spp;            // active rays, at positions [0, n)
     uint32_t Lcur = p.C;         // last_active_chunk (ray_tracing.rs:386)
-    uint64_t nseg = 0;
+    uint64_t nseg = 0, nslots = 0, niter = 0;
     for (uint32_t k = 0; k < depth; ++k) {
         bool act[S], surv[S];
 #pragma unroll
@@ -246,6 +278,8 @@ __global__ __launch_bounds__(1024) void trace_pixels(KParams<T> p) {
             }
         }
         nseg += n;
+        nslots += 64u * ((n + 63u) / 64u);
+        ++niter;
         unsigned long long bal[S];
 #pragma unroll
         for (int j = 0; j < S; ++j) {
@@ -311,7 +345,12 @@ __global__ __launch_bounds__(1024) void trace_pixels(KParams<T> p) {
         if (p.rgb) p.rgb[(size_t)b * 3 + tid] = q8(v);
         if (p.lin) p.lin[(size_t)b * 3 + tid] = (double)v;
     }
-    if (tid == 0) atomicAdd(&p.segs[(b & (kSegShards - 1)) * kSegStride], (unsigned long long)nseg);
+    if (tid == 0) {
+        unsigned long long* c = &p.segs[(b & (kSegShards - 1)) * kSegStride];
+        atomicAdd(c + 0, (unsigned long long)nseg);
+        atomicAdd(c + 1, (unsigned long long)nslots);
+        atomicAdd(c + 2, (unsigned long long)niter);
+    }
 }
 
 }  // namespace rt
@@ -561,14 +600,20 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
     HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
     HIPCHK(hipMemset(c->err, 0, 16));
-    uint64_t total = 0;
-    for (int i = 0; i < kSegShards; ++i) total += segs[(size_t)i * kSegStride];
+    uint64_t total = 0, slots = 0, iters = 0;
+    for (int i = 0; i < kSegShards; ++i) {
+        total += segs[(size_t)i * kSegStride];
+        slots += segs[(size_t)i * kSegStride + 1];
+        iters += segs[(size_t)i * kSegStride + 2];
+    }
     if (out) {
         memset(out, 0, sizeof(*out));
         out->kernel_ms = ms;
         out->pixels = c->pixels;
         out->samples = c->samples;
         out->ray_segments = total;
+        out->lane_slots = slots;
+        out->bounce_iters = iters;
     }
     c->have_first = false;
     c->pixels = c->samples = 0;

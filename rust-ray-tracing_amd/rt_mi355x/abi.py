@@ -57,6 +57,8 @@ class RtStats(ctypes.Structure):
         ("pixels", u64),
         ("samples", u64),
         ("ray_segments", u64),
+        ("lane_slots", u64),
+        ("bounce_iters", u64),
     ]
 
 
