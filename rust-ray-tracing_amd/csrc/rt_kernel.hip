@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <chrono>
@@ -69,19 +70,36 @@ template <typename T> struct KParams {
     double* lin;
     unsigned long long* segs;  // kSegShards counters, one per 128-B line
     uint32_t* err;
+    uint32_t* counter;         // next work item (pixel of the tile range)
+    uint32_t n_items;
+    char* scratch;             // per-wave scratch regions
+    size_t scratch_stride;
 };
 
 constexpr int kSegShards = 256;
+constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
+constexpr int kWavesF64 = 6;
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
 // Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
 // wave-uniform, so these become s_load into SGPRs — a free broadcast to all 64 lanes.
 template <typename T> using cptr = const __attribute__((address_space(4))) T*;
 
+// Cold kernel arguments (the camera) are read through an opaque pointer to the kernarg segment
+// at their point of use: otherwise the backend hoists every kernarg load to the kernel entry and
+// keeps ~40 camera SGPRs live across the whole persistent loop (SGPR spills into VGPR lanes).
+template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args() {
+    cptr<KParams<T>> k = (cptr<KParams<T>>)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    return k;
+}
+
 // Camera::get_ray, ray_tracing.rs:77-89 (jitter stream 0, disk stream 1).
 template <typename T>
-__device__ __forceinline__ void camera_ray(const KParams<T>& p, uint32_t col, uint32_t row, uint32_t pix,
+__device__ __forceinline__ void camera_ray(const KParams<T>& p0, uint32_t col, uint32_t row, uint32_t pix,
                                            uint32_t s, V3<T>& o, V3<T>& d) {
+    cptr<KParams<T>> pk = cold_args<T>();
+    const auto& p = *pk;
     const U4 r = philox(s, pix, 0u, 0u, p.k0, p.k1);
     const T xo = u01a(r, T(0)), yo = u01b(r, T(0));
     const T s1 = ((T)col + xo) / (T)p.W;
@@ -118,7 +136,9 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
         const T hb = pk_dot(oc, d);                                // :255
         const T c = pk_len2(oc) - s.r2;                            // :256
         const T disc = fma(hb, hb, -a * c);                        // :257
-        if (disc >= T(0.0)) {                                      // :259-261
+        // :259-261.  Exact pre-filter: with hb >= 0, root1 = (-hb - sd)*inv_a <= 0 can never be
+        // valid, so only Q1-off (root2) mode needs those lanes.
+        if (disc >= T(0.0) && (root2 || hb < T(0.0))) {
             const T sd = sqrt(disc);
             const T r1 = (-hb - sd) * inv_a;                       // :270
             bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
@@ -150,8 +170,9 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
         test(s, i);
     }
     if (best < 0) return false;      // sky: ray_tracing.rs:421-424
+    const auto& q = *cold_args<T>();
     // PackedHitRecords::finalize (objects.rs:157-162); normal = at_t(t) - center (:279-280)
-    const T* sg = p.sph + 4 * best;
+    const T* sg = q.sph + 4 * best;
     const V3<T> cen = mk(sg[0], sg[1], sg[2]);
     const V3<T> hp = mk(o.x + d.x * best_t, o.y + d.y * best_t, o.z + d.z * best_t);
     V3<T> nrm = sub(hp, cen);
@@ -160,8 +181,8 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     const bool front = pk_dot(d, nrm) < T(0.0);
     if (!front) nrm = neg(nrm);
     // Material::get_hit_result (materials.rs:54-147); scatter stream 2
-    const MatT<T> m = p.mats[p.smat[best]];
-    const U4 r = philox(sid, pix, k, 2u, p.k0, p.k1);
+    const MatT<T> m = q.mats[q.smat[best]];
+    const U4 r = philox(sid, pix, k, 2u, q.k0, q.k1);
     V3<T> nd;
     if (m.kind == RT_LAMBERTIAN) {
         nd = add(unit_vec(u01a(r, T(0)), u01b(r, T(0))), nrm);
@@ -192,164 +213,181 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     return true;
 }
 
-template <typename T> struct Smem {
-    T *ox, *oy, *oz, *dx, *dy, *dz, *cr, *cg, *cb;  // active-ray state by position
-    T *vr, *vg, *vb;                                 // retired value by position
-    T* yv;                                           // primary-ray y by position (Q2)
-    uint32_t* sid;                                   // sample id by position (RNG key)
-    uint32_t* wcnt;                                  // survivors per (slot, wave) group
-    T* part;                                         // 12 partial sums
+// Per-wave scratch in global memory (L2 / Infinity-Cache resident): SoA arrays of capacity P,
+// addressed as (wave-uniform base in SGPRs) + (field * P + position) * sizeof(T), so the loads
+// and stores use the SGPR-base + VGPR-offset form and no per-field pointer occupies registers.
+enum Field : uint32_t {
+    F_OX, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_CR, F_CG, F_CB,   // active rays by position
+    F_TR, F_TG, F_TB,                                         // rays terminated this bounce, by terminated rank
+    F_VR, F_VG, F_VB,                                         // retired value by position
+    F_YV,                                                     // primary-ray y by position (quirk Q2)
+    F_NT                                                      // number of T fields; then 2 u32 fields:
+};
+// u32 fields after the T fields: sample id by position (RNG key), old position of terminated rays.
+constexpr uint32_t U_SID = 0, U_TPOS = 1;
+
+__host__ __device__ inline size_t scratch_bytes(uint32_t P, size_t tsz) {
+    return ((size_t)P * (F_NT * tsz + 8) + 255) & ~(size_t)255;
+}
+
+template <typename T> struct Scratch {
+    char* base;
+    uint32_t P;
+    __device__ __forceinline__ T& f(uint32_t field, uint32_t i) const {
+        return *(T*)(base + ((size_t)field * P + i) * sizeof(T));
+    }
+    __device__ __forceinline__ uint32_t& u(uint32_t field, uint32_t i) const {
+        return *(uint32_t*)(base + (size_t)F_NT * P * sizeof(T) + ((size_t)field * P + i) * 4u);
+    }
 };
 
-__host__ __device__ inline size_t smem_bytes(uint32_t P, size_t tsz) {
-    return (size_t)P * (13 * tsz + 4) + 64 * 4 + 16 * tsz;
-}
+// Make this wave's earlier global stores visible to its later loads (other lanes, same wave).
+__device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <typename T>
-__device__ __forceinline__ Smem<T> carve(char* base, uint32_t P) {
-    Smem<T> s;
-    T* t = (T*)base;
-    s.ox = t; t += P; s.oy = t; t += P; s.oz = t; t += P;
-    s.dx = t; t += P; s.dy = t; t += P; s.dz = t; t += P;
-    s.cr = t; t += P; s.cg = t; t += P; s.cb = t; t += P;
-    s.vr = t; t += P; s.vg = t; t += P; s.vb = t; t += P;
-    s.yv = t; t += P;
-    s.part = t; t += 16;
-    uint32_t* u = (uint32_t*)t;
-    s.sid = u; u += P;
-    s.wcnt = u;
-    return s;
-}
+// One wave renders one pixel at a time (persistent; pixels pulled from an atomic counter).
+// Per bounce k the n_k active rays sit at positions [0, n_k) of the wave's scratch; the wave
+// walks them in rounds of 64 (lane = position within the round), traces each against all
+// spheres, and compacts survivors in place with __ballot/popcount: a survivor's new position
+// (its rank) never exceeds its old one, and rounds run in order, so no position is overwritten
+// before it is read.  Terminated rays are appended to a dense list; once n_{k+1} is known,
+// their retire-rule values are written into the position-indexed value array.
+template <typename T, int W>
+__global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
+    // Only the sphere-loop operands come from the by-value `p` (hoisted to SGPRs); everything
+    // else is re-read through cold_args() where it is used, to keep SGPR pressure low.
+    __shared__ unsigned long long wcount[4][3];   // per-wave work counters
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
+    if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
 
-template <typename T, int S>
-__global__ __launch_bounds__(1024) void trace_pixels(KParams<T> p) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const uint32_t NT = blockDim.x;
-    const uint32_t NW = NT >> 6;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6, lane = tid & 63u;
-    const uint32_t P = p.P, spp = p.spp, depth = p.depth;
-    Smem<T> sm = carve<T>(smem_raw, P);
+    for (;;) {
+        const auto& q = *cold_args<T>();
+        uint32_t item = 0;
+        if (lane == 0) item = atomicAdd(q.counter, 1u);
+        item = __builtin_amdgcn_readfirstlane(item);
+        if (item >= q.n_items) break;
+        const uint32_t ri = item / q.col_count, ci = item % q.col_count;
+        const uint32_t row = q.row_begin + ri * q.row_step, col = q.col_begin + ci;
+        const uint32_t pix = row * q.W + col;
+        const uint32_t P = q.P, spp = q.spp, depth = q.depth, C = q.C;
+        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+        const Scratch<T> sc{q.scratch + (size_t)gw * q.scratch_stride, P};
 
-    const uint32_t b = blockIdx.x;
-    const uint32_t ri = b / p.col_count, ci = b % p.col_count;
-    const uint32_t row = p.row_begin + ri * p.row_step, col = p.col_begin + ci;
-    const uint32_t pix = row * p.W + col;
-
-    // Retired-value array init.  Positions [spp, P) are the missing lanes of a partial last
-    // chunk: disabled from the start (ray.rs:140-144), hit_sky at bounce 0 (:421-424), zero
-    // primary direction -> sky(0); with depth 0 they keep white in buffer 0 (s_sel==0).
-    {
-        const V3<T> s0 = sky(T(0.0));
-        for (uint32_t q = tid; q < P; q += NT) {
-            T vr = 0, vg = 0, vb = 0;
-            if (q >= spp) {
-                if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
-                else if (p.s_sel == 0u) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
-            }
-            sm.vr[q] = vr; sm.vg[q] = vg; sm.vb[q] = vb;
-        }
-    }
-
-    V3<T> ro[S], rd[S], rc[S];
-    uint32_t rs[S];
-    uint32_t n = spp;            // active rays, at positions [0, n)
-    uint32_t Lcur = p.C;         // last_active_chunk (ray_tracing.rs:386)
-    uint64_t nseg = 0, nslots = 0, niter = 0;
-    for (uint32_t k = 0; k < depth; ++k) {
-        bool act[S], surv[S];
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            const uint32_t pos = (uint32_t)j * NT + tid;
-            act[j] = pos < n;
-            surv[j] = false;
-            if (act[j]) {
-                if (k == 0) {
-                    camera_ray(p, col, row, pix, pos, ro[j], rd[j]);
-                    rc[j] = mk(T(1.0), T(1.0), T(1.0));
-                    rs[j] = pos;
-                    sm.yv[pos] = rd[j].y;
-                } else {
-                    ro[j] = mk(sm.ox[pos], sm.oy[pos], sm.oz[pos]);
-                    rd[j] = mk(sm.dx[pos], sm.dy[pos], sm.dz[pos]);
-                    rc[j] = mk(sm.cr[pos], sm.cg[pos], sm.cb[pos]);
-                    rs[j] = sm.sid[pos];
+        // Retired-value init.  Positions [spp, P): missing lanes of a partial last chunk,
+        // disabled from the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424),
+        // zero primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel==0).
+        {
+            const V3<T> s0 = sky(T(0.0));
+            const bool white0 = q.s_sel == 0u;
+            for (uint32_t qi = lane; qi < P; qi += 64u) {
+                T vr = 0, vg = 0, vb = 0;
+                if (qi >= spp) {
+                    if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
+                    else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
                 }
-                surv[j] = bounce(p, ro[j], rd[j], rc[j], pix, rs[j], k);
+                sc.f(F_VR, qi) = vr; sc.f(F_VG, qi) = vg; sc.f(F_VB, qi) = vb;
             }
         }
-        nseg += n;
-        nslots += 64u * ((n + 63u) / 64u);
-        ++niter;
-        unsigned long long bal[S];
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            bal[j] = __ballot(act[j] && surv[j]);
-            if (lane == 0) sm.wcnt[j * NW + wave] = (uint32_t)__popcll(bal[j]);
-        }
-        __syncthreads();
-        uint32_t n_next = 0;
-        const uint32_t ng = (uint32_t)S * NW;
-        for (uint32_t g = 0; g < ng; ++g) n_next += sm.wcnt[g];
-        const uint32_t Lnext = (k + 1 == depth) ? 0u : (n_next + 3u) / 4u;
-        const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;
-        const bool U = p.s_sel == (k & 1u);   // final read hits this bounce's unsorted buffer
-#pragma unroll
-        for (int j = 0; j < S; ++j) {
-            if (!act[j]) continue;
-            const uint32_t pos = (uint32_t)j * NT + tid;
-            const uint32_t g = (uint32_t)j * NW + wave;
-            uint32_t base = 0;
-            for (uint32_t h = 0; h < g; ++h) base += sm.wcnt[h];
-            const uint32_t below = (uint32_t)__popcll(bal[j] & ((1ull << lane) - 1ull));
-            const uint32_t rank = base + below;   // survivors before `pos`
-            if (surv[j]) {
-                sm.ox[rank] = ro[j].x; sm.oy[rank] = ro[j].y; sm.oz[rank] = ro[j].z;
-                sm.dx[rank] = rd[j].x; sm.dy[rank] = rd[j].y; sm.dz[rank] = rd[j].z;
-                sm.cr[rank] = rc[j].x; sm.cg[rank] = rc[j].y; sm.cb[rank] = rc[j].z;
-                sm.sid[rank] = rs[j];
-            } else {
-                const uint32_t pnew = n_next + (pos - rank);
-                const bool old_in = pos >= lo && pos < hi;
-                const bool new_in = pnew >= lo && pnew < hi;
-                if (U && old_in) {
-                    const V3<T> s = sky(sm.yv[pos]);
-                    sm.vr[pos] = rc[j].x * s.x; sm.vg[pos] = rc[j].y * s.y; sm.vb[pos] = rc[j].z * s.z;
+
+        uint32_t n = spp;     // active rays, at positions [0, n)
+        uint32_t Lcur = C;    // last_active_chunk (ray_tracing.rs:386)
+        for (uint32_t k = 0; k < depth; ++k) {
+            uint32_t nsurv = 0;
+            for (uint32_t base = 0; base < n; base += 64u) {
+                const uint32_t pos = base + lane;
+                const bool act = pos < n;
+                bool surv = false;
+                V3<T> o, d, c;
+                uint32_t sid = 0;
+                if (act) {
+                    if (k == 0) {
+                        camera_ray(p, col, row, pix, pos, o, d);
+                        c = mk(T(1.0), T(1.0), T(1.0));
+                        sid = pos;
+                        sc.f(F_YV, pos) = d.y;
+                    } else {
+                        o = mk(sc.f(F_OX, pos), sc.f(F_OY, pos), sc.f(F_OZ, pos));
+                        d = mk(sc.f(F_DX, pos), sc.f(F_DY, pos), sc.f(F_DZ, pos));
+                        c = mk(sc.f(F_CR, pos), sc.f(F_CG, pos), sc.f(F_CB, pos));
+                        sid = sc.u(U_SID, pos);
+                    }
+                    surv = bounce(p, o, d, c, pix, sid, k);
                 }
-                if (!U || !new_in) {
-                    const V3<T> s = sky(sm.yv[pnew]);
-                    sm.vr[pnew] = rc[j].x * s.x; sm.vg[pnew] = rc[j].y * s.y; sm.vb[pnew] = rc[j].z * s.z;
+                const unsigned long long bal = __ballot(act && surv);
+                const uint32_t rank = nsurv + (uint32_t)__popcll(bal & lt_mask);
+                if (act) {
+                    if (surv) {   // stable compaction, ray_tracing.rs:430-458
+                        sc.f(F_OX, rank) = o.x; sc.f(F_OY, rank) = o.y; sc.f(F_OZ, rank) = o.z;
+                        sc.f(F_DX, rank) = d.x; sc.f(F_DY, rank) = d.y; sc.f(F_DZ, rank) = d.z;
+                        sc.f(F_CR, rank) = c.x; sc.f(F_CG, rank) = c.y; sc.f(F_CB, rank) = c.z;
+                        sc.u(U_SID, rank) = sid;
+                    } else {      // hit the sky (:421-424): keep colour + old position
+                        const uint32_t t = pos - rank;
+                        sc.f(F_TR, t) = c.x; sc.f(F_TG, t) = c.y; sc.f(F_TB, t) = c.z;
+                        sc.u(U_TPOS, t) = pos;
+                    }
+                }
+                nsurv += (uint32_t)__popcll(bal);
+            }
+            if (lane == 0) {
+                wcount[wave][0] += n;
+                wcount[wave][1] += 64u * ((n + 63u) / 64u);
+                wcount[wave][2] += 1u;
+            }
+            const auto& q2 = *cold_args<T>();
+            const uint32_t n_next = nsurv, nterm = n - nsurv;
+            const uint32_t Lnext = (k + 1 == q2.depth) ? 0u : (n_next + 3u) / 4u;
+            const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;   // positions retiring at bounce k
+            const bool U = q2.s_sel == (k & 1u);                // final read = this bounce's unsorted buffer
+            wave_mem_sync();
+            for (uint32_t t0 = 0; t0 < nterm; t0 += 64u) {
+                const uint32_t t = t0 + lane;
+                if (t < nterm) {
+                    const uint32_t pold = sc.u(U_TPOS, t), pnew = n_next + t;
+                    const V3<T> c = mk(sc.f(F_TR, t), sc.f(F_TG, t), sc.f(F_TB, t));
+                    if (U && pold >= lo && pold < hi) {
+                        const V3<T> s = sky(sc.f(F_YV, pold));
+                        sc.f(F_VR, pold) = c.x * s.x; sc.f(F_VG, pold) = c.y * s.y; sc.f(F_VB, pold) = c.z * s.z;
+                    }
+                    if (!U || pnew < lo || pnew >= hi) {
+                        const V3<T> s = sky(sc.f(F_YV, pnew));
+                        sc.f(F_VR, pnew) = c.x * s.x; sc.f(F_VG, pnew) = c.y * s.y; sc.f(F_VB, pnew) = c.z * s.z;
+                    }
                 }
             }
+            wave_mem_sync();
+            n = n_next;
+            Lcur = Lnext;
+            if (n == 0) break;
         }
-        __syncthreads();
-        n = n_next;
-        Lcur = Lnext;
-        if (n == 0) break;
-    }
 
-    // Final reduction in the reference's order: per lane l, sum chunks j = 0..C-1 from +0.0
-    // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
-    if (tid < 12) {
-        const uint32_t ch = tid >> 2, l = tid & 3u;
-        const T* v = ch == 0 ? sm.vr : (ch == 1 ? sm.vg : sm.vb);
+        // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
+        // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
         T acc = T(0.0);
-        for (uint32_t j = 0; j < p.C; ++j) acc = acc + v[4 * j + l];
-        sm.part[tid] = acc;
+        if (lane < 12u) {
+            const uint32_t ch = lane >> 2, l = lane & 3u;
+            for (uint32_t j = 0; j < C; ++j) acc = acc + sc.f(F_VR + ch, 4 * j + l);
+        }
+        const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
+                s3 = __shfl(acc, (int)((lane + 3) & 63u));
+        if (lane < 12u && (lane & 3u) == 0u) {
+            const uint32_t ch = lane >> 2;
+            const T tot = (((T(0.0) + acc) + s1) + s2) + s3;
+            const T v = tot / (T)spp;                                   // renderer.rs:161
+            const auto& q3 = *cold_args<T>();
+            if (!(v <= T(2.0))) atomicOr(q3.err, 1u);                   // color.rs:55-57 assert
+            if (q3.rgb) q3.rgb[(size_t)item * 3 + ch] = q8(v);
+            if (q3.lin) q3.lin[(size_t)item * 3 + ch] = (double)v;
+        }
     }
-    __syncthreads();
-    if (tid < 3) {
-        const T* s4 = sm.part + 4 * tid;
-        const T tot = (((T(0.0) + s4[0]) + s4[1]) + s4[2]) + s4[3];
-        const T v = tot / (T)spp;                                   // renderer.rs:161
-        if (!(v <= T(2.0))) atomicOr(p.err, 1u);                    // color.rs:55-57 assert
-        if (p.rgb) p.rgb[(size_t)b * 3 + tid] = q8(v);
-        if (p.lin) p.lin[(size_t)b * 3 + tid] = (double)v;
-    }
-    if (tid == 0) {
-        unsigned long long* c = &p.segs[(b & (kSegShards - 1)) * kSegStride];
-        atomicAdd(c + 0, (unsigned long long)nseg);
-        atomicAdd(c + 1, (unsigned long long)nslots);
-        atomicAdd(c + 2, (unsigned long long)niter);
+    if (lane == 0) {
+        const auto& q = *cold_args<T>();
+        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+        unsigned long long* c = &q.segs[(gw & (kSegShards - 1)) * kSegStride];
+        atomicAdd(c + 0, wcount[wave][0]);
+        atomicAdd(c + 1, wcount[wave][1]);
+        atomicAdd(c + 2, wcount[wave][2]);
     }
 }
 
@@ -381,6 +419,10 @@ struct rt_context {
     uint32_t n_spheres = 0, n_materials = 0;
     unsigned long long* segs = nullptr;
     uint32_t* err = nullptr;
+    uint32_t* counter = nullptr;   // persistent-kernel work counter (zeroed before each launch)
+    void* scratch = nullptr;       // per-wave ray state (grown on demand)
+    size_t scratch_bytes = 0;
+    int n_cu = 0;
     uint64_t samples = 0, pixels = 0;
 };
 
@@ -434,6 +476,8 @@ extern "C" int rt_context_create(int device, rt_context** out) {
     HIPCHK(hipEventCreate(&c->ev_last));
     HIPCHK(hipMalloc((void**)&c->segs, sizeof(unsigned long long) * kSegShards * kSegStride));
     HIPCHK(hipMalloc((void**)&c->err, 16));
+    HIPCHK(hipMalloc((void**)&c->counter, 16));
+    HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHK(hipMemset(c->segs, 0, sizeof(unsigned long long) * kSegShards * kSegStride));
     HIPCHK(hipMemset(c->err, 0, 16));
     *out = c;
@@ -453,7 +497,7 @@ extern "C" int rt_context_destroy(rt_context* c) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     free_scene(c);
-    (void)hipFree(c->segs); (void)hipFree(c->err);
+    (void)hipFree(c->segs); (void)hipFree(c->err); (void)hipFree(c->counter); (void)hipFree(c->scratch);
     (void)hipEventDestroy(c->ev_first); (void)hipEventDestroy(c->ev_last);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -518,9 +562,11 @@ static bool check_range(const rt_camera* cam, const rt_tile_range* r) {
     return last_row < cam->image_height;
 }
 
-template <typename T, int S>
+static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
+
+template <typename T>
 static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_t spp, uint64_t seed, uint32_t flags,
-                    const rt_tile_range& rg, void* d_rgb, void* d_lin, hipStream_t st, uint32_t NT, size_t lds) {
+                    const rt_tile_range& rg, void* d_rgb, void* d_lin, hipStream_t st) {
     KParams<T> p;
     memset(&p, 0, sizeof(p));
     const bool f64 = sizeof(T) == 8;
@@ -545,11 +591,40 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.lin = (double*)d_lin;
     p.segs = c->segs;
     p.err = c->err;
-    auto kern = trace_pixels<T, S>;
-    HIPCHK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    const uint64_t nblocks = (uint64_t)rg.row_count * rg.col_count;
-    hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3(NT), lds, st, p);
+    p.counter = c->counter;
+    p.n_items = rg.row_count * rg.col_count;
+
+    // Persistent grid: as many 4-wave workgroups as stay resident, never more waves than pixels.
+    // Minimum waves per SIMD the register allocation targets (RT_WAVES overrides; experiments).
+    static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
+    const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
+    void (*kern)(KParams<T>) = W >= 8 ? trace_waves<T, 8> : W >= 6 ? trace_waves<T, 6> : W >= 5 ? trace_waves<T, 5>
+                             : W >= 4 ? trace_waves<T, 4> : W >= 3 ? trace_waves<T, 3> : trace_waves<T, 1>;
+    int per_cu = 0;
+    HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));
+    if (per_cu < 1) per_cu = 1;
+    uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
+    const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
+    if (nblocks > need) nblocks = need;
+    p.scratch_stride = scratch_bytes(p.P, sizeof(T));
+    const int rc = ensure_scratch(c, p.scratch_stride * nblocks * 4, st);
+    if (rc != RT_OK) return rc;
+    p.scratch = (char*)c->scratch;
+    HIPCHK(hipMemsetAsync(c->counter, 0, sizeof(uint32_t), st));
+    hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3(256), 0, st, p);
     HIPCHK(hipGetLastError());
+    return RT_OK;
+}
+
+static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st) {
+    if (bytes <= c->scratch_bytes) return RT_OK;
+    HIPCHK(hipStreamSynchronize(st));
+    HIPCHK(hipDeviceSynchronize());
+    if (c->scratch) HIPCHK(hipFree(c->scratch));
+    c->scratch = nullptr;
+    c->scratch_bytes = 0;
+    HIPCHK(hipMalloc(&c->scratch, bytes));
+    c->scratch_bytes = bytes;
     return RT_OK;
 }
 
@@ -557,29 +632,21 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
                                uint32_t flags, const rt_tile_range* range, void* d_rgb8, void* d_linear, void* stream) {
     if (!c || !cam) return fail(RT_ERR_INVALID, "rt_render_async: NULL argument");
     if (spp == 0) return fail(RT_ERR_INVALID, "rt_render_async: spp == 0 (the reference panics: 0/0 in to_u8_array)");
+    if (spp > (1u << 20)) return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp > 2^20");
     if (cam->image_width == 0 || cam->image_height == 0) return fail(RT_ERR_INVALID, "rt_render_async: empty image");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "image too large");
     rt_tile_range rg = range ? *range : rt_tile_range{0, 1, cam->image_height, 0, cam->image_width};
     if (!check_range(cam, &rg)) return fail(RT_ERR_INVALID, "rt_render_async: tile range outside the image");
     if ((uint64_t)rg.row_count * rg.col_count > 0x7FFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "too many pixels in one call");
-    const uint32_t C = (spp + 3) / 4, P = 4 * C;
-    uint32_t NT = P < 1024 ? ((P + 63) / 64) * 64 : 1024;
-    const uint32_t S = (P + NT - 1) / NT;
     const bool f32 = (flags & RT_FLAG_F32) != 0;
-    const size_t lds = smem_bytes(P, f32 ? 4 : 8);
-    if (S > 2 || lds > 160 * 1024)
-        return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp too large for the per-pixel LDS budget in this precision");
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if (!c->have_first) {
         HIPCHK(hipEventRecord(c->ev_first, st));
         c->have_first = true;
     }
-    int rc;
-    if (f32) rc = S == 1 ? launch_t<float, 1>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds)
-                         : launch_t<float, 2>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds);
-    else rc = S == 1 ? launch_t<double, 1>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds)
-                     : launch_t<double, 2>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st, NT, lds);
+    const int rc = f32 ? launch_t<float>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st)
+                       : launch_t<double>(c, cam, max_bounces, spp, seed, flags, rg, d_rgb8, d_linear, st);
     if (rc != RT_OK) return rc;
     HIPCHK(hipEventRecord(c->ev_last, st));
     c->pixels += (uint64_t)rg.row_count * rg.col_count;

@@ -92,9 +92,14 @@ def test_large_spp(renderer, scene_100):
     assert_parity(renderer, scene_100, cam_for(8, 6), 50, 2048, abi.RT_FLAG_F32)  # two slots per thread
 
 
-def test_fp64_2048_unsupported(renderer, scene_100):
+def test_fp64_2048(renderer, scene_100):
+    """Config E's spp in fp64 (per-wave scratch has no LDS ceiling)."""
+    assert_parity(renderer, scene_100, cam_for(4, 3), 50, 2048, 0)
+
+
+def test_spp_limit(renderer, scene_100):
     with pytest.raises(rt.RtError) as e:
-        gpu(renderer, scene_100, cam_for(8, 6), 50, 2048, flags=0)
+        gpu(renderer, scene_100, cam_for(2, 2), 50, (1 << 20) + 1, flags=abi.RT_FLAG_F32)
     assert e.value.code == abi.RT_ERR_UNSUPPORTED
 
 
