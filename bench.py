@@ -104,10 +104,9 @@ def main():
     abi.check(lib, lib.rt_context_create(local_rank, ctypes.byref(ctx)))
     abi.check(lib, lib.rt_context_set_scene(ctx, ctypes.byref(flat.abi)))
 
-    rows = len(range(rank, H, world))
-    rows_max = (H + world - 1) // world
-    tile = abi.RtTileRange(rank, world, rows, 0, W)
-    shard = torch.zeros((rows_max, W, 3), dtype=torch.uint8, device="cuda")
+    from rt_mi355x import parallel
+    tile = parallel.shard_range(W, H, world, rank)
+    shard = torch.zeros((parallel.rows_max(H, world), W, 3), dtype=torch.uint8, device="cuda")
     gathered = [torch.empty_like(shard) for _ in range(world)] if (world > 1 and rank == 0) else None
     image = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     stream = torch.cuda.current_stream()
@@ -119,10 +118,7 @@ def main():
         if world > 1:
             dist.gather(shard, gathered, dst=0)
             if rank == 0:
-                st = torch.stack(gathered)                      # [N, rows_max, W, 3]
-                for r in range(world):
-                    nr = len(range(r, H, world))
-                    image[r::world] = st[r, :nr]
+                parallel.assemble_rows(gathered, H, world, image)
         elif rank == 0:
             image.copy_(shard[:H])
 

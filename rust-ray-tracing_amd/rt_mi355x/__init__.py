@@ -8,8 +8,9 @@ from .abi import load_library, RtError
 from .scene import Camera, Dielectric, FlatScene, Lambertian, Metal, Scene, Sphere, MAIN_CAMERA, camera_new_py
 from .renderer import GpuRenderer, RenderStat, Renderer
 from . import scenes
+from . import parallel
 
 __all__ = [
     "abi", "load_library", "RtError", "Camera", "Dielectric", "FlatScene", "Lambertian", "Metal", "Scene",
-    "Sphere", "MAIN_CAMERA", "camera_new_py", "GpuRenderer", "RenderStat", "Renderer", "scenes",
+    "Sphere", "MAIN_CAMERA", "camera_new_py", "GpuRenderer", "RenderStat", "Renderer", "scenes", "parallel",
 ]

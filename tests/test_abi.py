@@ -1,0 +1,121 @@
+"""The drop-in C ABI (include/rt_mi355x.h): the HIP library loads, exports every declared symbol,
+and its struct layouts match what a C compiler sees.  No GPU compute here."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import rt_mi355x as rt
+from rt_mi355x import abi
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "rt_mi355x.h")
+
+
+def _ensure_built():
+    if not os.path.exists(abi.LIB_PATH):
+        subprocess.run(["make", "-C", os.path.join(REPO, "rust-ray-tracing_amd")], check=True, capture_output=True)
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(rt_\w+)\s*\(", text, flags=re.M)))
+
+
+def test_header_declares_the_abi():
+    fns = declared_functions()
+    assert sorted(abi.EXPORTED) == fns
+
+
+def test_library_exports_every_symbol():
+    _ensure_built()
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (rt_\w+)$", out, flags=re.M))
+    assert set(declared_functions()) <= exported
+
+
+def test_library_is_gfx950_only():
+    """The fat binary carries exactly one code object, for gfx950 (no CUDA/dual path)."""
+    _ensure_built()
+    blob = open(abi.LIB_PATH, "rb").read()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa--(gfx[0-9a-z]+)", blob))
+    assert targets == {b"gfx950"}
+    assert b"nvptx" not in blob
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "rt_mi355x.h"
+#define P(T, F) printf(#T "." #F " %zu\n", offsetof(T, F));
+int main(void) {
+  printf("rt_material %zu\nrt_scene %zu\nrt_camera %zu\nrt_tile_range %zu\nrt_stats %zu\n",
+         sizeof(rt_material), sizeof(rt_scene), sizeof(rt_camera), sizeof(rt_tile_range), sizeof(rt_stats));
+  P(rt_material, albedo) P(rt_material, fuzz) P(rt_material, ior)
+  P(rt_scene, center) P(rt_scene, radius) P(rt_scene, material) P(rt_scene, materials)
+  P(rt_camera, center) P(rt_camera, ulc) P(rt_camera, dv)
+  P(rt_stats, kernel_ms) P(rt_stats, ray_segments) P(rt_stats, bounce_iters)
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_c(tmp_path):
+    src = tmp_path / "layout.c"
+    src.write_text(C_LAYOUT)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), "-o", str(exe), str(src)], check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                               check=True).stdout.splitlines())
+    py = {
+        "rt_material": ctypes.sizeof(abi.RtMaterial), "rt_scene": ctypes.sizeof(abi.RtScene),
+        "rt_camera": ctypes.sizeof(abi.RtCamera), "rt_tile_range": ctypes.sizeof(abi.RtTileRange),
+        "rt_stats": ctypes.sizeof(abi.RtStats),
+    }
+    for k, v in py.items():
+        assert int(got[k]) == v, k
+    for key, val in got.items():
+        if "." in key:
+            st, field = key.split(".")
+            cls = {"rt_material": abi.RtMaterial, "rt_scene": abi.RtScene, "rt_camera": abi.RtCamera,
+                   "rt_stats": abi.RtStats}[st]
+            assert getattr(cls, field).offset == int(val), key
+
+
+def test_host_only_entry_points():
+    """rt_camera_new / rt_metal_clamp_fuzz / rt_version are pure host code."""
+    _ensure_built()
+    lib = rt.load_library()
+    assert lib.rt_version().startswith(b"rt_mi355x")
+    assert lib.rt_metal_clamp_fuzz(5.0) == 1.0 and lib.rt_metal_clamp_fuzz(0.25) == 0.25
+    cam = rt.Camera(1920, 1080, **rt.MAIN_CAMERA, lib=lib)
+    py = rt.camera_new_py(1920, 1080, **rt.MAIN_CAMERA)
+    for f in ("center", "ulc", "vu", "vv", "du", "dv"):
+        assert list(getattr(cam.abi, f)) == list(getattr(py, f)), f
+    assert list(cam.abi.ulc) == [5.734425819985221, 3.855608886593495, 13.912440284912917]
+    D3 = ctypes.c_double * 3
+    bad = abi.RtCamera()
+    assert lib.rt_camera_new(ctypes.byref(bad), 0, 10, 10.0, 30.0, D3(0, 0, 0), D3(0, 0, 1), D3(0, 1, 0), 0.0) \
+        == abi.RT_ERR_INVALID
+    assert b"bad argument" in lib.rt_last_error()
+
+
+def test_no_gpu_fails_loudly():
+    """Without a GPU the library reports an error instead of falling back to the CPU."""
+    _ensure_built()
+    lib = rt.load_library()
+    ctx = ctypes.c_void_p()
+    rc = lib.rt_context_create(0, ctypes.byref(ctx))
+    if rc == abi.RT_OK:
+        lib.rt_context_destroy(ctx)
+        pytest.skip("GPU present")
+    assert rc in (abi.RT_ERR_HIP, abi.RT_ERR_INVALID)
+    assert lib.rt_last_error()
+    with pytest.raises(rt.RtError):
+        rt.GpuRenderer(lib=lib)

@@ -175,3 +175,59 @@ def test_renderer_trait(renderer):
     img, stat = renderer.render(8, 16, scene, cam)
     assert img.shape == (30, 40, 3) and img.dtype == np.uint8
     assert stat.pixels_rendered() == 1200 and stat.pixels_per_second() > 0
+
+
+# ---------------------------------------------------------------- committed golden fixtures
+import os  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _golden_cases():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    return mg
+
+
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz")))
+def test_golden_fixtures_gpu(renderer, name):
+    mg = _golden_cases()
+    tag, w, h, depth, spp, flags, prec, _ = mg.CASES[name]
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    flat = mg.scene_for(tag)
+    cam = cam_for(w, h)
+    f = flags | (abi.RT_FLAG_F32 if prec == "f32" else 0)
+    rgb, lin, st, rc = gpu(renderer, flat, cam, depth, spp, int(g["seed"]), f)
+    assert rc == 0
+    np.testing.assert_array_equal(rgb.reshape(h, w, 3), g["rgb8"])
+    assert st.ray_segments == int(g["segments"])
+    if "linear" in g:
+        np.testing.assert_array_equal(lin.reshape(h, w, 3), g["linear"])
+
+
+# ---------------------------------------------------------------- BASELINE sizes
+@pytest.mark.parametrize("config,flags", [("B", abi.RT_FLAG_F32), ("C", abi.RT_FLAG_F32), ("C", 0)])
+def test_full_size_configs(renderer, config, flags):
+    """Configs B and C at their full BASELINE sizes: deterministic across launches, the two-shard
+    row partition reassembles the frame bit-exactly, and a strided pixel subset is bit-identical
+    to the oracle (which cannot render the whole frame in test time)."""
+    w, h, n_sph, spp, depth = rt.scenes.CONFIGS[config]
+    flat = rt.scenes.config_scene(config).flatten()
+    cam = cam_for(w, h)
+    rgb, lin, st, rc = gpu(renderer, flat, cam, depth, spp, SEED, flags)
+    assert rc == 0
+    rgb2, lin2, st2, _ = gpu(renderer, flat, cam, depth, spp, SEED, flags)
+    np.testing.assert_array_equal(lin, lin2)
+    assert st.ray_segments == st2.ray_segments
+    img = lin.reshape(h, w, 3)
+    for r in range(2):
+        part = gpu(renderer, flat, cam, depth, spp, SEED, flags,
+                   tile=rt.parallel.shard_range(w, h, 2, r))[1]
+        np.testing.assert_array_equal(part.reshape(-1, w, 3), img[r::2])
+    px = (np.arange(48, dtype=np.int64) * 43201) % (w * h)
+    _, lin_o, _, _ = oracle_render(flat, cam, depth, spp, SEED, 0, pixels=px.astype(np.uint32),
+                                   precision="f32" if flags & abi.RT_FLAG_F32 else "f64")
+    np.testing.assert_array_equal(lin[px], lin_o)
+    assert 0.2 < lin.mean() < 0.9 and 1.0 < st.ray_segments / (w * h * spp) < 4.0

@@ -1,0 +1,318 @@
+"""Pin the CPU oracle (test infrastructure) with known answers derived from the reference source.
+
+The reference has no tests/fixtures and cannot be built, so the pins are:
+published Philox4x32-10 vectors (Random123), hand-derived Camera::new values, Color::to_u8_array's
+table, and semantic properties of the packed path (empty scene, Q1 inside-sphere, tie rule,
+hollow-dielectric mirror, Q3 buffer read).  RNG-stream parity with the real binary is unpinned
+(thread_rng is unseedable); see oracle/oracle.h.
+"""
+import ctypes
+import math
+import os
+
+import numpy as np
+import pytest
+
+import rt_mi355x as rt
+from rt_mi355x import abi
+from oracle_bind import load_oracle, oracle_render
+
+SEED = 0x5EED0001
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def philox(ctr, key):
+    lib = load_oracle()
+    out = (ctypes.c_uint32 * 4)()
+    lib.oracle_philox4x32_10((ctypes.c_uint32 * 4)(*ctr), (ctypes.c_uint32 * 2)(*key), out)
+    return list(out)
+
+
+def test_philox_published_kats():
+    # Random123 kat_vectors, philox4x32 R=10
+    assert philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    assert philox([0xFFFFFFFF] * 4, [0xFFFFFFFF] * 2) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_camera_new_kat():
+    """Camera::new for src/main.rs:51-58 at 16:9 (ray_tracing.rs:27-62), hand-derived values."""
+    lib = load_oracle()
+    cam = abi.RtCamera()
+    D3 = ctypes.c_double * 3
+    assert lib.oracle_camera_new(ctypes.addressof(cam), 1920, 1080, 10.0, 30.0, D3(16, 2, 18.5), D3(0, 0, 0),
+                                 D3(0, 1, 0), 0.0) == 0
+    vh = -cam.vv[1] / math.sqrt(1 - 0)  # vv = -v * vh, v.y component is the dominant one
+    assert math.isclose(math.sqrt(sum(x * x for x in cam.vu)), 9.527082397551029, rel_tol=1e-15)
+    assert math.isclose(math.sqrt(sum(x * x for x in cam.vv)), 5.358983848622454, rel_tol=1e-15)
+    assert list(cam.ulc) == [5.734425819985221, 3.855608886593495, 13.912440284912917]
+    assert list(cam.du) == [0.0, 0.0, -0.0] or all(x == 0.0 for x in cam.du)
+    assert vh > 0
+    # the Python restatement agrees bit-for-bit
+    py = rt.camera_new_py(1920, 1080, **rt.MAIN_CAMERA)
+    for f in ("center", "ulc", "vu", "vv", "du", "dv"):
+        assert list(getattr(py, f)) == list(getattr(cam, f)), f
+
+
+def test_centre_ray_and_sky():
+    """Image-centre primary direction (-0.65198, -0.08150, -0.75385) -> sky (0.77037, 0.86222, 1.0)."""
+    lib = load_oracle()
+    cam = rt.camera_new_py(1920, 1080, **rt.MAIN_CAMERA)
+    o, d = (ctypes.c_double * 3)(), (ctypes.c_double * 3)()
+    lib.oracle_get_ray_f64(ctypes.addressof(cam), 960, 540, 0, SEED, o, d)
+    assert list(o) == [16.0, 2.0, 18.5]
+    np.testing.assert_allclose(list(d), [-0.65198, -0.08150, -0.75385], atol=2e-3)
+    assert math.isclose(math.sqrt(sum(x * x for x in d)), 1.0, rel_tol=1e-15)
+    a = (d[1] + 1.0) * 0.5
+    sky = [(1 - a) + 0.5 * a, (1 - a) + 0.7 * a, (1 - a) + 1.0 * a]
+    np.testing.assert_allclose(sky, [0.77037, 0.86222, 1.0], atol=1e-3)
+
+
+@pytest.mark.parametrize("v,expect,panic", [
+    (0.0, 0, 0), (1.0, 255, 0), (0.25, 127, 0), (0.5, 181, 0), (2.0, 255, 0),
+    (2.0000001, 255, 1), (float("nan"), 0, 1), (-1.0, 0, 0), (1e-12, 0, 0),
+])
+def test_to_u8_table(v, expect, panic):
+    """Color::to_u8_array (color.rs:54-64): (sqrt(c)*255.999) as u8, saturating; assert c <= 2.0."""
+    lib = load_oracle()
+    out = (ctypes.c_uint8 * 3)()
+    p = ctypes.c_int(0)
+    lib.oracle_to_u8((ctypes.c_double * 3)(v, v, v), out, ctypes.byref(p))
+    assert list(out) == [expect] * 3
+    assert p.value == panic
+
+
+def test_sincos_polynomial_accuracy():
+    lib = load_oracle()
+    rng = np.random.default_rng(1)
+    s, c = ctypes.c_double(), ctypes.c_double()
+    worst = 0.0
+    for u in np.concatenate([rng.random(4000), [0.0, 0.125, 0.25, 0.5, 0.75, 0.999999999]]):
+        lib.oracle_sincos2pi_f64(float(u), ctypes.byref(s), ctypes.byref(c))
+        worst = max(worst, abs(s.value - math.sin(2 * math.pi * u)), abs(c.value - math.cos(2 * math.pi * u)))
+        assert abs(s.value * s.value + c.value * c.value - 1.0) < 1e-15
+    assert worst < 2e-15
+    lib.oracle_sincos2pi_f64(0.25, ctypes.byref(s), ctypes.byref(c))
+    assert (s.value, c.value) == (1.0, 0.0) or abs(c.value) < 1e-16
+
+
+def test_empty_scene_is_mean_sky():
+    """hitables = []: every sample misses at bounce 0 -> pixel = mean sky(primary y), summed in the
+    reference's order (per lane over chunks, then lanes).  Restated here in Python doubles."""
+    lib = load_oracle()
+    flat = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((1, 1, 1))])
+    w, h, spp = 12, 7, 10
+    cam = rt.camera_new_py(w, h, **rt.MAIN_CAMERA)
+    _, lin, segs, rc = oracle_render(flat, cam, 8, spp, SEED)
+    assert rc == 0 and segs == w * h * spp
+    C = (spp + 3) // 4
+    o, d = (ctypes.c_double * 3)(), (ctypes.c_double * 3)()
+    for row in range(h):
+        for col in range(w):
+            ys = []
+            for s in range(4 * C):
+                if s < spp:
+                    lib.oracle_get_ray_f64(ctypes.addressof(cam), col, row, s, SEED, o, d)
+                    ys.append(d[1])
+                else:
+                    ys.append(0.0)          # missing lane of the partial chunk: zero direction
+            lanes = []
+            for ch in range(3):
+                acc = [0.0] * 4
+                for j in range(C):
+                    for l in range(4):
+                        a = (ys[4 * j + l] + 1.0) * 0.5
+                        sky = ((-a + 1.0) * 1.0 + a * 0.5, (-a + 1.0) * 1.0 + a * 0.7, (-a + 1.0) * 1.0 + a * 1.0)[ch]
+                        acc[l] = acc[l] + 1.0 * sky
+                lanes.append(((((0.0 + acc[0]) + acc[1]) + acc[2]) + acc[3]) / spp)
+            assert lanes == list(lin[row * w + col]), (row, col)
+
+
+def _one_sphere(center, radius, mat):
+    return rt.FlatScene(np.array([center], float), np.array([radius], float), np.array([0], np.uint32), [mat])
+
+
+def test_q1_inside_sphere_never_hits():
+    """Q1 (objects.rs:273): a ray starting inside a sphere never hits its far side, so a camera
+    inside a huge sphere sees sky; with the scalar semantics (ROOT2) it sees the sphere."""
+    inside = _one_sphere((0, 0, 0), 1000.0, rt.Lambertian((0.5, 0.5, 0.5)))
+    empty = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((1, 1, 1))])
+    cam = rt.camera_new_py(16, 9, **rt.MAIN_CAMERA)
+    _, lin_q1, _, _ = oracle_render(inside, cam, 8, 8, SEED)
+    _, lin_e, _, _ = oracle_render(empty, cam, 8, 8, SEED)
+    _, lin_r2, _, _ = oracle_render(inside, cam, 8, 8, SEED, flags=abi.RT_FLAG_ROOT2)
+    np.testing.assert_array_equal(lin_q1, lin_e)
+    assert lin_r2.mean() < 0.8 * lin_e.mean()
+
+
+def test_tie_later_sphere_wins():
+    """PackedHitRecords::update uses t <= best (objects.rs:141): of two identical spheres the later wins."""
+    red, blue = rt.Lambertian((0.9, 0.1, 0.1)), rt.Lambertian((0.1, 0.1, 0.9))
+    both = rt.FlatScene(np.array([[0, 0, 0], [0, 0, 0]], float), np.array([4.0, 4.0]), np.array([0, 1], np.uint32),
+                        [red, blue])
+    only_blue = _one_sphere((0, 0, 0), 4.0, blue)
+    cam = rt.camera_new_py(16, 9, **rt.MAIN_CAMERA)
+    _, a, _, _ = oracle_render(both, cam, 8, 8, SEED)
+    _, b, _, _ = oracle_render(only_blue, cam, 8, 8, SEED)
+    np.testing.assert_array_equal(a, b)
+
+
+def test_hollow_dielectric_is_mirror():
+    """Hollow dielectric under Q1: cos(theta) < 0 -> Schlick > 1 -> always reflects."""
+    hollow = _one_sphere((0, 0, 0), 4.0, rt.Dielectric(1.5, True))
+    mirror = _one_sphere((0, 0, 0), 4.0, rt.Metal((1.0, 1.0, 1.0), 0.0))
+    cam = rt.camera_new_py(16, 9, **rt.MAIN_CAMERA)
+    _, a, _, _ = oracle_render(hollow, cam, 8, 8, SEED)
+    _, b, _, _ = oracle_render(mirror, cam, 8, 8, SEED)
+    np.testing.assert_allclose(a, b, rtol=0, atol=1e-15)
+
+
+def test_metal_fuzz_clamp():
+    """Metal::new clamps fuzz to <= 1 (materials.rs:79-88) but not below 0."""
+    assert rt.Metal((1, 1, 1), 5.0).fuzzy_factor == 1.0
+    assert rt.Metal((1, 1, 1), 0.3).fuzzy_factor == 0.3
+    assert rt.Metal((1, 1, 1), -0.5).fuzzy_factor == -0.5
+    assert rt.Metal((1, 1, 1), 1.0).fuzzy_factor == 1.0
+
+
+def test_oracle_threads_deterministic():
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(24, 14, **rt.MAIN_CAMERA)
+    r1 = oracle_render(flat, cam, 50, 12, SEED, threads=1)
+    r8 = oracle_render(flat, cam, 50, 12, SEED, threads=8)
+    np.testing.assert_array_equal(r1[1], r8[1])
+    assert r1[2] == r8[2]
+
+
+def test_pixel_subset_matches_full():
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(20, 10, **rt.MAIN_CAMERA)
+    _, full, _, _ = oracle_render(flat, cam, 50, 8, SEED)
+    px = np.array([0, 7, 55, 199, 120], np.uint32)
+    _, sub, _, _ = oracle_render(flat, cam, 50, 8, SEED, pixels=px)
+    np.testing.assert_array_equal(sub, full[px])
+
+
+def test_fp32_tracks_fp64_statistically():
+    """fp32 mode vs the reference's fp64 arithmetic: per-channel image mean within 0.5 % and
+    per-pixel RMSE below the Monte-Carlo noise of the fp64 image (the fp32 tolerance we state)."""
+    flat = rt.scenes.random_spheres(500).flatten()
+    cam = rt.camera_new_py(48, 27, **rt.MAIN_CAMERA)
+    _, l64, _, _ = oracle_render(flat, cam, 50, 64, SEED)
+    _, l32, _, _ = oracle_render(flat, cam, 50, 64, SEED, precision="f32")
+    _, l64b, _, _ = oracle_render(flat, cam, 50, 64, SEED + 1)
+    m64, m32 = l64.mean(0), l32.mean(0)
+    assert np.all(np.abs(m32 - m64) / m64 < 5e-3)
+    rmse = np.sqrt(((l32 - l64) ** 2).mean())
+    noise = np.sqrt(((l64b - l64) ** 2).mean())   # two independent fp64 renders
+    assert rmse < noise
+
+
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz")))
+def test_golden_fixtures(name):
+    """The oracle reproduces every committed golden fixture bit-for-bit (drift guard)."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    g = np.load(os.path.join(GOLDEN, name + ".npz"))
+    rgb, lin, segs = mg.render_case(name)
+    np.testing.assert_array_equal(rgb, g["rgb8"])
+    assert segs == int(g["segments"])
+    if "linear" in g:
+        np.testing.assert_array_equal(lin, g["linear"])
+
+
+# ---------------------------------------------------------------------------------------------
+# Quirk Q3 (ray_tracing.rs:486): pure-Python model check of the kernel's retire rule against the
+# literal two-buffer algorithm, on random termination patterns (no geometry).
+# ---------------------------------------------------------------------------------------------
+def _literal(spp, depth, alive, att, ysky):
+    """trace_vectorized2's buffer logic; alive[k][sample], att[k][sample] = per-bounce attenuation."""
+    C = (spp + 3) // 4
+    P = 4 * C
+    en = [[s < spp for s in range(P)], [True] * P]
+    sid = [list(range(P)), [0] * P]
+    col = [[1.0] * P, [1.0] * P]
+    sky = [[False] * P, [False] * P]
+    last = C
+    for k in range(depth):
+        if last == 0:
+            break
+        sel = k % 2
+        for q in range(4 * last):
+            if en[sel][q]:
+                s = sid[sel][q]
+                if alive[k][s]:
+                    col[sel][q] = col[sel][q] * att[k][s]
+                else:
+                    en[sel][q] = False
+                    sky[sel][q] = True
+            else:
+                sky[sel][q] = True
+        ns = 1 - sel
+        order = [q for q in range(4 * last) if en[sel][q]] + [q for q in range(4 * last) if not en[sel][q]]
+        n_en = sum(1 for q in range(4 * last) if en[sel][q])
+        for dst, src in enumerate(order):
+            en[ns][dst], sid[ns][dst], col[ns][dst], sky[ns][dst] = en[sel][src], sid[sel][src], col[sel][src], sky[sel][src]
+        last = (n_en + 3) // 4
+    S = (C - 1) % 2
+    vals = []
+    for q in range(P):
+        v = col[S][q] * ysky[q] if sky[S][q] else col[S][q]
+        vals.append(0.0 if en[S][q] else v)
+    return vals
+
+
+def _retire_rule(spp, depth, alive, att, ysky):
+    """The kernel's formulation (rt_kernel.hip trace_waves): positions retire at bounce k in
+    [4*L_{k+1}, 4*L_k); each terminated ray writes its value at its old position (if the final
+    read hits this bounce's unsorted buffer and that position retires now) and/or at its new
+    position (otherwise, or if the new position retires later)."""
+    C = (spp + 3) // 4
+    P = 4 * C
+    S = (C - 1) % 2
+    vals = [0.0] * P
+    for q in range(spp, P):
+        vals[q] = ysky[q] if depth > 0 else (1.0 if S == 0 else 0.0)
+    rays = [(s, 1.0) for s in range(spp)]   # active rays in position order
+    Lcur = C
+    for k in range(depth):
+        n = len(rays)
+        surv, term = [], []
+        for pos, (s, c) in enumerate(rays):
+            if alive[k][s]:
+                surv.append((s, c * att[k][s]))
+            else:
+                term.append((pos, c))
+        n_next = len(surv)
+        Lnext = 0 if k + 1 == depth else (n_next + 3) // 4
+        lo, hi = 4 * Lnext, 4 * Lcur
+        U = S == k % 2
+        for t, (pold, c) in enumerate(term):
+            pnew = n_next + t
+            if U and lo <= pold < hi:
+                vals[pold] = c * ysky[pold]
+            if not U or not (lo <= pnew < hi):
+                vals[pnew] = c * ysky[pnew]
+        rays = surv
+        Lcur = Lnext
+        if not rays:
+            break
+    return vals
+
+
+@pytest.mark.parametrize("trial", range(300))
+def test_q3_retire_rule_matches_literal(trial):
+    rng = np.random.default_rng(trial)
+    spp = int(rng.integers(1, 40))
+    depth = int(rng.integers(0, 9))
+    p_alive = rng.uniform(0.1, 0.95)
+    P = 4 * ((spp + 3) // 4)
+    alive = rng.random((max(depth, 1), P)) < p_alive
+    att = rng.uniform(0.1, 1.0, (max(depth, 1), P))
+    ysky = list(rng.uniform(0.5, 1.0, P))
+    for q in range(spp, P):
+        ysky[q] = 0.777   # sky(0) stand-in for the zero-direction lanes
+    assert _literal(spp, depth, alive, att, ysky) == _retire_rule(spp, depth, alive, att, ysky)
