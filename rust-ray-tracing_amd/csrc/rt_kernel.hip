@@ -29,6 +29,7 @@
 
 #include <chrono>
 #include <cmath>
+#include <limits>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -43,22 +44,32 @@ template <typename T> struct MatT {
     T ar, ag, ab, fuzz, ior;
 };
 
-template <typename T> struct alignas(4 * sizeof(T)) SphT { T cx, cy, cz, r2; };
-template <typename T> struct alignas(64) SphGroup { SphT<T> s[64 / sizeof(SphT<T>)]; };
+// Device sphere layout (rt_context_set_scene): 64-byte groups, one s_load_dwordx16 each, padded
+// with never-hit dummies (r^2 = -inf makes the discriminant -inf) to whole groups.
+//   fp32: 4 spheres per group as 2 pair-interleaved records {cx0,cx1, cy0,cy1, cz0,cz1, r0,r1}
+//         so each quantity of a sphere pair is an adjacent SGPR pair for packed-FP32 VALU ops;
+//   fp64: 2 spheres per group as {cx, cy, cz, r^2}.
+// A separate AoS table {cx, cy, cz, r^2} per sphere serves the per-lane finalize gather.
+template <typename T> constexpr uint32_t kGroup = 64 / (4 * sizeof(T));
+template <typename T> struct alignas(64) SphGroup { T v[64 / sizeof(T)]; };
 
 // One 64-byte scalar load worth of spheres (s_load_dwordx16 into SGPRs).
 template <typename T>
 __device__ __forceinline__ SphGroup<T> load_group(const __attribute__((address_space(4))) T* f, uint32_t g) {
     constexpr int NE = 64 / sizeof(T);
     SphGroup<T> r;
-    T* out = &r.s[0].cx;
 #pragma unroll
-    for (int e = 0; e < NE; ++e) out[e] = f[g * NE + e];
+    for (int e = 0; e < NE; ++e) r.v[e] = f[g * NE + e];
     return r;
 }
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <typename T> struct KParams {
-    const T* sph;              // [n][4] = cx, cy, cz, r*r (r.powi(2), objects.rs:256) in T
+    const T* sph;              // grouped sphere records (layout above); r^2 = r.powi(2) in T (objects.rs:256)
+    const T* cen;              // [n][4] = cx, cy, cz, r^2 (AoS, finalize gather)
+    uint32_t n_groups;
     const uint32_t* smat;      // [n] material index
     const MatT<T>* mats;
     uint32_t n_spheres;
@@ -77,8 +88,9 @@ template <typename T> struct KParams {
 };
 
 constexpr int kSegShards = 256;
-constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
-constexpr int kWavesF64 = 6;
+constexpr int kWavesF32 = 8;   // default min-waves-per-SIMD targets (measured sweep)
+constexpr int kWavesF64 = 5;
+constexpr int kWavesRoot2 = 8;  // the Q1-off (scalar semantics) variant
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
 // Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
@@ -119,60 +131,114 @@ __device__ __forceinline__ void camera_ray(const KParams<T>& p0, uint32_t col, u
     d = unit(sub(pc, orig));
 }
 
+// Walk the sphere groups with a two-deep scalar-load pipeline over two SGPR buffers (no
+// per-group SGPR copies).  Scalar loads return out of order, so any use waits lgkmcnt(0): the
+// next group's load is pinned (sched_barrier) BEFORE the current group's math and waited right
+// after it, so it is always one whole group of VALU work old when it is consumed.  The device
+// buffer holds a dummy group past the end, so the prefetches never need clamping.
+template <typename T, typename F>
+__device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
+    SphGroup<T> A = load_group(f, 0);
+    uint32_t g = 0;
+    for (; g + 1 < ng; g += 2) {
+        const SphGroup<T> B = load_group(f, g + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        group(A, g);
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): B has landed
+        __builtin_amdgcn_sched_barrier(0);
+        A = load_group(f, g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        group(B, g + 1);
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // A has landed
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g < ng) group(A, g);
+}
+
 // One bounce of one enabled ray: the object loop of trace_vectorized2 (ray_tracing.rs:399-403)
 // + the per-lane material step (:406-426).  Returns true if the ray hit (and was scattered).
-template <typename T>
+template <typename T, bool root2>
 __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, V3<T>& col, uint32_t pix,
                                        uint32_t sid, uint32_t k) {
     const T a = pk_len2(d);          // objects.rs:253
     const T inv_a = T(1.0) / a;      // objects.rs:254 (loop-invariant)
     T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
     int best = -1;
-    const bool root2 = (p.flags & RT_FLAG_ROOT2) != 0u;
-    const uint32_t n = p.n_spheres;
     // Sphere::hit_packed (objects.rs:249-290) + PackedHitRecords::update (objects.rs:140-155)
-    auto test = [&](const SphT<T>& s, uint32_t i) {
-        const V3<T> oc = mk(o.x - s.cx, o.y - s.cy, o.z - s.cz);   // :252
-        const T hb = pk_dot(oc, d);                                // :255
-        const T c = pk_len2(oc) - s.r2;                            // :256
-        const T disc = fma(hb, hb, -a * c);                        // :257
-        // :259-261.  Exact pre-filter: with hb >= 0, root1 = (-hb - sd)*inv_a <= 0 can never be
-        // valid, so only Q1-off (root2) mode needs those lanes.
-        if (disc >= T(0.0) && (root2 || hb < T(0.0))) {
-            const T sd = sqrt(disc);
-            const T r1 = (-hb - sd) * inv_a;                       // :270
-            bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
-            T root = r1;
-            if (root2 && !valid) {                                 // Q1 off: scalar semantics
-                root = (-hb + sd) * inv_a;                         // :271
-                valid = root >= T(0.001) && root < T(INFINITY);
-            }
-            if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
+    // for a candidate whose discriminant is non-negative.  Exact pre-filter: with hb >= 0,
+    // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
+    auto hit = [&](T hb, T disc, uint32_t i) {
+        const T sd = sqrt(disc);
+        const T r1 = (-hb - sd) * inv_a;                       // :270
+        bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
+        T root = r1;
+        if (root2 && !valid) {                                 // Q1 off: scalar semantics
+            root = (-hb + sd) * inv_a;                         // :271
+            valid = root >= T(0.001) && root < T(INFINITY);
         }
+        if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
     };
-    // Spheres stream through the scalar cache in 64-byte groups (4 x f32 or 2 x f64 spheres =
-    // one s_load_dwordx16); group g+1 is requested before group g is tested so the K$ latency
-    // hides behind G*13 VALU ops.
-    constexpr uint32_t G = 64 / sizeof(SphT<T>);
+    // Spheres stream through the scalar cache in 64-byte groups; group g+1 is requested before
+    // group g is tested so the K$ latency hides behind the group's VALU work.
+    // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
     cptr<T> f = (cptr<T>)__builtin_assume_aligned(p.sph, 64);
-    const uint32_t ng = n / G;
-    if (ng > 0) {
-        SphGroup<T> cur = load_group(f, 0);
-        for (uint32_t g = 0; g < ng; ++g) {
-            const SphGroup<T> nxt = load_group(f, g + 1 < ng ? g + 1 : g);
+    const uint32_t ng = p.n_groups;
+    // Candidate filter, branch-free: m = min(disc, -hb) >= 0 holds whenever disc >= 0 && hb < 0
+    // (the only case in which root1 can be valid); its false positives (hb == 0, NaN) are
+    // rejected again inside hit(), so the filter never changes a result.  One wave-level branch
+    // per 64-byte group keeps the scalar unit (shared by the CU's 4 SIMDs) off the critical path.
+    auto cand = [&](T hb, T disc) -> T { return root2 ? disc : fmin(disc, -hb); };
+    if constexpr (sizeof(T) == 4) {
+        // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two spheres,
+        // so the results are bit-identical to the scalar sequence (:252-257).
+        const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+        const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+        const f2 na = {-a, -a};
+        auto group = [&](const SphGroup<T>& cur, uint32_t g) {
+            f2 hb[2], disc[2];
 #pragma unroll
-            for (uint32_t j = 0; j < G; ++j) test(cur.s[j], g * G + j);
-            cur = nxt;
-        }
-    }
-    for (uint32_t i = ng * G; i < n; ++i) {
-        const SphT<T> s{f[4 * i + 0], f[4 * i + 1], f[4 * i + 2], f[4 * i + 3]};
-        test(s, i);
+            for (uint32_t q = 0; q < 2; ++q) {
+                const T* v = &cur.v[8 * q];
+                const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
+                const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
+                hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));                   // :255
+                const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;      // :256
+                disc[q] = fma2(hb[q], hb[q], na * c);                             // :257
+            }
+            const T m0 = cand(hb[0].x, disc[0].x), m1 = cand(hb[0].y, disc[0].y);
+            const T m2 = cand(hb[1].x, disc[1].x), m3 = cand(hb[1].y, disc[1].y);
+            if (fmax(fmax(m0, m1), fmax(m2, m3)) >= T(0.0)) {
+                const uint32_t i0 = 4 * g;
+                if (m0 >= T(0.0)) hit(hb[0].x, disc[0].x, i0);
+                if (m1 >= T(0.0)) hit(hb[0].y, disc[0].y, i0 + 1);
+                if (m2 >= T(0.0)) hit(hb[1].x, disc[1].x, i0 + 2);
+                if (m3 >= T(0.0)) hit(hb[1].y, disc[1].y, i0 + 3);
+            }
+        };
+        sphere_loop(f, ng, group);
+    } else {
+        auto group = [&](const SphGroup<T>& cur, uint32_t g) {
+            T hb[2], disc[2];
+#pragma unroll
+            for (uint32_t j = 0; j < 2; ++j) {
+                const T* v = &cur.v[4 * j];
+                const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
+                hb[j] = pk_dot(oc, d);                                     // :255
+                const T c = pk_len2(oc) - v[3];                            // :256
+                disc[j] = fma(hb[j], hb[j], -a * c);                       // :257
+            }
+            const T m0 = cand(hb[0], disc[0]), m1 = cand(hb[1], disc[1]);
+            if (fmax(m0, m1) >= T(0.0)) {
+                if (m0 >= T(0.0)) hit(hb[0], disc[0], 2 * g);
+                if (m1 >= T(0.0)) hit(hb[1], disc[1], 2 * g + 1);
+            }
+        };
+        sphere_loop(f, ng, group);
     }
     if (best < 0) return false;      // sky: ray_tracing.rs:421-424
     const auto& q = *cold_args<T>();
     // PackedHitRecords::finalize (objects.rs:157-162); normal = at_t(t) - center (:279-280)
-    const T* sg = q.sph + 4 * best;
+    const T* sg = q.cen + 4 * best;
     const V3<T> cen = mk(sg[0], sg[1], sg[2]);
     const V3<T> hp = mk(o.x + d.x * best_t, o.y + d.y * best_t, o.z + d.z * best_t);
     V3<T> nrm = sub(hp, cen);
@@ -251,7 +317,7 @@ __device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(
 // (its rank) never exceeds its old one, and rounds run in order, so no position is overwritten
 // before it is read.  Terminated rays are appended to a dense list; once n_{k+1} is known,
 // their retire-rule values are written into the position-indexed value array.
-template <typename T, int W>
+template <typename T, int W, bool ROOT2>
 __global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
     // Only the sphere-loop operands come from the by-value `p` (hoisted to SGPRs); everything
     // else is re-read through cold_args() where it is used, to keep SGPR pressure low.
@@ -312,7 +378,7 @@ __global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
                         c = mk(sc.f(F_CR, pos), sc.f(F_CG, pos), sc.f(F_CB, pos));
                         sid = sc.u(U_SID, pos);
                     }
-                    surv = bounce(p, o, d, c, pix, sid, k);
+                    surv = bounce<T, ROOT2>(p, o, d, c, pix, sid, k);
                 }
                 const unsigned long long bal = __ballot(act && surv);
                 const uint32_t rank = nsurv + (uint32_t)__popcll(bal & lt_mask);
@@ -413,7 +479,9 @@ struct rt_context {
     hipEvent_t ev_first = nullptr, ev_last = nullptr;
     bool have_first = false;
     // scene, fp64 and fp32 images
-    void* sph64 = nullptr; void* sph32 = nullptr;
+    void* sph64 = nullptr; void* sph32 = nullptr;   // grouped sphere records
+    void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
+    uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
     uint32_t* smat = nullptr;
     uint32_t n_spheres = 0, n_materials = 0;
@@ -486,8 +554,9 @@ extern "C" int rt_context_create(int device, rt_context** out) {
 
 static void free_scene(rt_context* c) {
     (void)hipFree(c->sph64); (void)hipFree(c->sph32); (void)hipFree(c->mat64); (void)hipFree(c->mat32);
+    (void)hipFree(c->cen64); (void)hipFree(c->cen32);
     (void)hipFree(c->smat);
-    c->sph64 = c->sph32 = c->mat64 = c->mat32 = nullptr;
+    c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
     c->n_spheres = c->n_materials = 0;
 }
@@ -504,15 +573,34 @@ extern "C" int rt_context_destroy(rt_context* c) {
     return RT_OK;
 }
 
+// Grouped, padded sphere records (layout at SphGroup) + AoS centre table, in precision T.
 template <typename T>
-static void pack_scene(const rt_scene* s, std::vector<T>& sph, std::vector<MatT<T>>& mats) {
-    sph.resize((size_t)4 * (s->n_spheres ? s->n_spheres : 1));
-    for (uint32_t i = 0; i < s->n_spheres; ++i) {
+static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& cen, std::vector<MatT<T>>& mats,
+                       uint32_t& n_groups) {
+    const uint32_t G = kGroup<T>;
+    const uint32_t n = s->n_spheres;
+    n_groups = (n + G - 1) / G;
+    const uint32_t npad = n_groups * G;
+    cen.assign((size_t)4 * (n ? n : 1), T(0));
+    for (uint32_t i = 0; i < n; ++i) {
         const T r = (T)s->radius[i];
-        sph[4 * i + 0] = (T)s->center[3 * i + 0];
-        sph[4 * i + 1] = (T)s->center[3 * i + 1];
-        sph[4 * i + 2] = (T)s->center[3 * i + 2];
-        sph[4 * i + 3] = r * r;   // self.radius.powi(2) in T (objects.rs:256)
+        cen[4 * i + 0] = (T)s->center[3 * i + 0];
+        cen[4 * i + 1] = (T)s->center[3 * i + 1];
+        cen[4 * i + 2] = (T)s->center[3 * i + 2];
+        cen[4 * i + 3] = r * r;   // self.radius.powi(2) in T (objects.rs:256)
+    }
+    auto field = [&](uint32_t i, int f) -> T {   // dummies: centre 0, r^2 = -inf (never hit)
+        if (i >= n) return f == 3 ? -std::numeric_limits<T>::infinity() : T(0);
+        return cen[4 * i + f];
+    };
+    grp.assign((size_t)64 / sizeof(T) * (n_groups + 1), T(0));   // + 1 dummy group: prefetch target
+    for (uint32_t i = 0; i < npad + G; ++i) {
+        const uint32_t g = i / G, j = i % G;
+        T* out = &grp[(size_t)g * (64 / sizeof(T))];
+        for (int f = 0; f < 4; ++f) {
+            if (sizeof(T) == 4) out[8 * (j / 2) + 2 * f + (j % 2)] = field(i, f);   // pair-interleaved
+            else out[4 * j + f] = field(i, f);                                     // AoS
+        }
     }
     mats.resize(s->n_materials ? s->n_materials : 1);
     for (uint32_t i = 0; i < s->n_materials; ++i) {
@@ -534,22 +622,25 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     free_scene(c);
-    std::vector<double> s64; std::vector<MatT<double>> m64;
-    std::vector<float> s32; std::vector<MatT<float>> m32;
-    pack_scene(s, s64, m64);
-    pack_scene(s, s32, m32);
+    std::vector<double> g64, c64; std::vector<MatT<double>> m64;
+    std::vector<float> g32, c32; std::vector<MatT<float>> m32;
+    pack_scene(s, g64, c64, m64, c->n_groups64);
+    pack_scene(s, g32, c32, m32, c->n_groups32);
     std::vector<uint32_t> sm(s->n_spheres ? s->n_spheres : 1, 0);
     for (uint32_t i = 0; i < s->n_spheres; ++i) sm[i] = s->material[i];
-    HIPCHK(hipMalloc(&c->sph64, s64.size() * sizeof(double)));
-    HIPCHK(hipMalloc(&c->sph32, s32.size() * sizeof(float)));
-    HIPCHK(hipMalloc(&c->mat64, m64.size() * sizeof(MatT<double>)));
-    HIPCHK(hipMalloc(&c->mat32, m32.size() * sizeof(MatT<float>)));
-    HIPCHK(hipMalloc((void**)&c->smat, sm.size() * sizeof(uint32_t)));
-    HIPCHK(hipMemcpy(c->sph64, s64.data(), s64.size() * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->sph32, s32.data(), s32.size() * sizeof(float), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->mat64, m64.data(), m64.size() * sizeof(MatT<double>), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->mat32, m32.data(), m32.size() * sizeof(MatT<float>), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->smat, sm.data(), sm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    auto up = [&](void** dst, const void* src, size_t bytes) -> int {
+        HIPCHK(hipMalloc(dst, bytes));
+        HIPCHK(hipMemcpy(*dst, src, bytes, hipMemcpyHostToDevice));
+        return RT_OK;
+    };
+    int rc;
+    if ((rc = up(&c->sph64, g64.data(), g64.size() * sizeof(double))) != RT_OK) return rc;
+    if ((rc = up(&c->sph32, g32.data(), g32.size() * sizeof(float))) != RT_OK) return rc;
+    if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
+    if ((rc = up(&c->cen32, c32.data(), c32.size() * sizeof(float))) != RT_OK) return rc;
+    if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
+    if ((rc = up(&c->mat32, m32.data(), m32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
+    if ((rc = up((void**)&c->smat, sm.data(), sm.size() * sizeof(uint32_t))) != RT_OK) return rc;
     c->n_spheres = s->n_spheres;
     c->n_materials = s->n_materials;
     return RT_OK;
@@ -571,6 +662,8 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     memset(&p, 0, sizeof(p));
     const bool f64 = sizeof(T) == 8;
     p.sph = (const T*)(f64 ? c->sph64 : c->sph32);
+    p.cen = (const T*)(f64 ? c->cen64 : c->cen32);
+    p.n_groups = f64 ? c->n_groups64 : c->n_groups32;
     p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
     p.smat = c->smat;
     p.n_spheres = c->n_spheres;
@@ -598,8 +691,11 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // Minimum waves per SIMD the register allocation targets (RT_WAVES overrides; experiments).
     static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
     const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
-    void (*kern)(KParams<T>) = W >= 8 ? trace_waves<T, 8> : W >= 6 ? trace_waves<T, 6> : W >= 5 ? trace_waves<T, 5>
-                             : W >= 4 ? trace_waves<T, 4> : W >= 3 ? trace_waves<T, 3> : trace_waves<T, 1>;
+    const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
+    void (*kern)(KParams<T>) =
+        r2 ? trace_waves<T, kWavesRoot2, true>
+           : (W >= 8 ? trace_waves<T, 8, false> : W >= 6 ? trace_waves<T, 6, false> : W >= 5 ? trace_waves<T, 5, false>
+            : W >= 4 ? trace_waves<T, 4, false> : trace_waves<T, 1, false>);
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));
     if (per_cu < 1) per_cu = 1;
