@@ -87,9 +87,16 @@ def main():
     import torch   # imported before the HIP library so both share one HIP runtime
     import torch.distributed as dist
 
-    torch.cuda.set_device(local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    # One process per GPU.  RT_BENCH_BACKEND=gloo (rehearsal only: several ranks sharing one GPU,
+    # shards staged through host memory) exercises the same partition/gather/assembly code.
+    backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
+    if world > 1 or "RANK" in os.environ:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
 
     import rt_mi355x as rt
     from rt_mi355x import abi
@@ -101,7 +108,7 @@ def main():
     flags = abi.RT_FLAG_F32 if args.precision == "f32" else 0
 
     ctx = ctypes.c_void_p()
-    abi.check(lib, lib.rt_context_create(local_rank, ctypes.byref(ctx)))
+    abi.check(lib, lib.rt_context_create(device, ctypes.byref(ctx)))
     abi.check(lib, lib.rt_context_set_scene(ctx, ctypes.byref(flat.abi)))
 
     from rt_mi355x import parallel
@@ -116,7 +123,14 @@ def main():
         abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tile),
                                            ctypes.c_void_p(shard.data_ptr()), None, sptr))
         if world > 1:
-            dist.gather(shard, gathered, dst=0)
+            if backend == "nccl":   # RCCL over xGMI, device buffers
+                dist.gather(shard, gathered, dst=0)
+            else:
+                host = [g.cpu() for g in gathered] if rank == 0 else None
+                dist.gather(shard.cpu(), host, dst=0)
+                if rank == 0:
+                    for g, h in zip(gathered, host):
+                        g.copy_(h)
             if rank == 0:
                 parallel.assemble_rows(gathered, H, world, image)
         elif rank == 0:
@@ -145,7 +159,8 @@ def main():
     segs = st.ray_segments
     kernel_ms = st.kernel_ms
 
-    stats = torch.tensor([elapsed, float(segs), kernel_ms], dtype=torch.float64, device="cuda")
+    red_dev = "cuda" if backend == "nccl" else "cpu"
+    stats = torch.tensor([elapsed, float(segs), kernel_ms], dtype=torch.float64, device=red_dev)
     if world > 1:
         t_max = stats[0].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -189,7 +204,9 @@ def main():
                 "workload": f"{args.config}: {W}x{H}, {n_sph} spheres (RTIOW-style, seed 0x5EED0001), "
                             f"{spp} spp, {depth} bounces, camera of src/main.rs:51-58",
                 "width": W, "height": H, "spheres": n_sph, "spp": spp, "max_bounces": depth,
-                "parallelism": f"row-interleaved image shards x{world}" + (" + RCCL gather" if world > 1 else ""),
+                "parallelism": f"row-interleaved image shards x{world}"
+                               + ((" + RCCL gather" if backend == "nccl" else f" + {backend} gather (rehearsal)")
+                                  if world > 1 else ""),
             },
             "roofline": {
                 "bound": "valu",
@@ -213,8 +230,11 @@ def main():
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
 
+    if rank == 0 and os.environ.get("RT_BENCH_SAVE"):
+        import numpy as np
+        np.save(os.environ["RT_BENCH_SAVE"], image.cpu().numpy())
     lib.rt_context_destroy(ctx)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

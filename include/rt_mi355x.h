@@ -119,19 +119,20 @@ int rt_context_create(int device, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
 /* Upload (replace) the scene; copies fp64 and fp32 SoA images into HBM. */
 int rt_context_set_scene(rt_context* ctx, const rt_scene* scene);
-/* Enqueue one render on `stream` (hipStream_t, NULL = the context's own stream).
- * d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous. */
+/* Enqueue one render on `stream` (a hipStream_t; NULL = the HIP null stream, as in every HIP
+ * API).  d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous.  Renders on
+ * one context must be issued to one stream at a time (they share the context's work counter). */
 int rt_render_async(rt_context* ctx, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
                     uint64_t seed, uint32_t flags, const rt_tile_range* range, void* d_rgb8,
                     void* d_linear, void* stream);
-/* Synchronise `stream`, then report and reset the counters accumulated by the renders
+/* Synchronise `stream` (NULL = null stream), then report and reset the counters accumulated by the renders
  * enqueued since the last call (ray_segments, error flag).  kernel_ms = device time between
  * the first and last enqueued render (HIP events on that stream). */
 int rt_context_collect(rt_context* ctx, void* stream, rt_stats* stats);
 /* Device memory helpers (so hosts without a HIP toolchain can drive the async API). */
 int rt_device_alloc(rt_context* ctx, size_t bytes, void** out);
 int rt_device_free(rt_context* ctx, void* ptr);
-int rt_memcpy_d2h(rt_context* ctx, void* dst, const void* src, size_t bytes);
+int rt_memcpy_d2h(rt_context* ctx, void* dst, const void* src, size_t bytes);   /* synchronises the device */
 
 /* Last error message of the calling thread ("" if none). */
 const char* rt_last_error(void);

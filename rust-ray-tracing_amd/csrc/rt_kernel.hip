@@ -736,7 +736,7 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
     if ((uint64_t)rg.row_count * rg.col_count > 0x7FFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "too many pixels in one call");
     const bool f32 = (flags & RT_FLAG_F32) != 0;
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream
     if (!c->have_first) {
         HIPCHK(hipEventRecord(c->ev_first, st));
         c->have_first = true;
@@ -753,7 +753,7 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
 extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (!c) return fail(RT_ERR_INVALID, "rt_context_collect: NULL context");
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream
     HIPCHK(hipStreamSynchronize(st));
     std::vector<unsigned long long> segs(kSegShards * kSegStride);
     uint32_t err = 0;
@@ -799,7 +799,7 @@ extern "C" int rt_device_free(rt_context* c, void* ptr) {
 extern "C" int rt_memcpy_d2h(rt_context* c, void* dst, const void* src, size_t bytes) {
     if (!c || !dst || !src) return fail(RT_ERR_INVALID, "rt_memcpy_d2h: NULL argument");
     HIPCHK(hipSetDevice(c->device));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipDeviceSynchronize());
     HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
     return RT_OK;
 }
