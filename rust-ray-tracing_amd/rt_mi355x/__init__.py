@@ -9,8 +9,10 @@ from .scene import Camera, Dielectric, FlatScene, Lambertian, Metal, Scene, Sphe
 from .renderer import GpuRenderer, RenderStat, Renderer
 from . import scenes
 from . import parallel
+from . import toml_scene
+from .toml_scene import Panic, load_scene, scene_from_toml
 
 __all__ = [
     "abi", "load_library", "RtError", "Camera", "Dielectric", "FlatScene", "Lambertian", "Metal", "Scene",
-    "Sphere", "MAIN_CAMERA", "camera_new_py", "GpuRenderer", "RenderStat", "Renderer", "scenes", "parallel",
+    "Sphere", "MAIN_CAMERA", "camera_new_py", "GpuRenderer", "RenderStat", "Renderer", "scenes", "parallel", "toml_scene", "Panic", "load_scene", "scene_from_toml",
 ]
