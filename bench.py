@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores of this process")
     ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--max-spheres", type=int, default=0, help="experiment: truncate the scene (not a bench line)")
     return ap.parse_args()
 
 
@@ -103,7 +104,11 @@ def main():
 
     lib = rt.load_library()
     W, H, n_sph, spp, depth = rt.scenes.CONFIGS[args.config]
-    flat = rt.scenes.config_scene(args.config).flatten()
+    scene = rt.scenes.config_scene(args.config)
+    if args.max_spheres:
+        scene = rt.Scene.from_list(scene.objects[:args.max_spheres])
+        n_sph = len(scene.objects)
+    flat = scene.flatten()
     cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
     flags = abi.RT_FLAG_F32 if args.precision == "f32" else 0
 

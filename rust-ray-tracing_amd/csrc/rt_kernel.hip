@@ -88,9 +88,10 @@ template <typename T> struct KParams {
 };
 
 constexpr int kSegShards = 256;
-constexpr int kWavesF32 = 8;   // default min-waves-per-SIMD targets (measured sweep)
+constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
+constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
 constexpr int kWavesF64 = 5;
-constexpr int kWavesRoot2 = 8;  // the Q1-off (scalar semantics) variant
+constexpr int kWavesRoot2 = 6;  // the Q1-off (scalar semantics) variant
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
 // Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
@@ -119,7 +120,9 @@ __device__ __forceinline__ void camera_ray(const KParams<T>& p0, uint32_t col, u
     const V3<T> vu = mk(p.vu[0], p.vu[1], p.vu[2]), vv = mk(p.vv[0], p.vv[1], p.vv[2]);
     const V3<T> pc = add(mk(p.ulc[0], p.ulc[1], p.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
     T dx = 0, dy = 0;  // random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2
-    for (uint32_t i = 0; i < 256u; ++i) {
+    // With zero defocus vectors and no -0.0 in the camera centre, du*dx + dv*dy + center == center
+    // for every finite disk sample, so the draw cannot change a bit of the result: skip it.
+    for (uint32_t i = 0; i < (p.flags & kFlagPinholeInternal ? 0u : 256u); ++i) {
         const U4 q = philox(s, pix, i, 1u, p.k0, p.k1);
         const T x = T(2.0) * u01a(q, T(0)) - T(1.0);
         const T y = T(2.0) * u01b(q, T(0)) - T(1.0);
@@ -433,7 +436,16 @@ __global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
         T acc = T(0.0);
         if (lane < 12u) {
             const uint32_t ch = lane >> 2, l = lane & 3u;
-            for (uint32_t j = 0; j < C; ++j) acc = acc + sc.f(F_VR + ch, 4 * j + l);
+            // loads in batches of 16 (independent addresses in flight), adds strictly in order
+            uint32_t j = 0;
+            for (; j + 16 <= C; j += 16) {
+                T v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = sc.f(F_VR + ch, 4 * (j + u) + l);
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc = acc + v[u];
+            }
+            for (; j < C; ++j) acc = acc + sc.f(F_VR + ch, 4 * j + l);
         }
         const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
                 s3 = __shfl(acc, (int)((lane + 3) & 63u));
@@ -677,6 +689,14 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.P = 4 * p.C;
     p.depth = depth;
     p.flags = flags;
+    {
+        bool pinhole = true;
+        for (int i = 0; i < 3; ++i) {
+            if (p.du[i] != T(0) || p.dv[i] != T(0)) pinhole = false;
+            if (p.center[i] == T(0) && std::signbit(p.center[i])) pinhole = false;
+        }
+        if (pinhole) p.flags |= kFlagPinholeInternal;
+    }
     p.s_sel = (p.C - 1) % 2;   // ray_tracing.rs:486
     p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32);
     p.row_begin = rg.row_begin; p.row_step = rg.row_step; p.col_begin = rg.col_begin; p.col_count = rg.col_count;
