@@ -250,3 +250,11 @@ def test_cli_renders_config_a_from_toml(tmp_path):
         assert "Viewport Top Left Corner: [5.734425819985221, 3.855608886593495, 13.912440284912917]" in r.stdout
         img = np.asarray(Image.open(tmp_path / out).convert("RGB"))
         np.testing.assert_array_equal(img, want)
+
+
+@pytest.mark.parametrize("flags,spp", [(abi.RT_FLAG_F32, 2048), (0, 256)])
+def test_config_e_scene(renderer, flags, spp):
+    """Config E's 10 000-sphere scene (2 500 scalar-load groups per ray) at config E's spp (fp32)."""
+    flat = rt.scenes.config_scene("E").flatten()
+    assert flat.n_spheres == 10000
+    assert_parity(renderer, flat, cam_for(4, 3), 50, spp, flags)
