@@ -11,10 +11,6 @@ PREC=${2:-f32}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 STEPS=5
-timeout -k 10 300 python3 bench.py --precision "$PREC" --steps $STEPS > "$OUT/bench.log" 2>&1 || exit $?
-grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- \
-    python3 bench.py --precision "$PREC" --steps $STEPS --cpu-seconds 0 > "$OUT/ktrace.log" 2>&1 || exit $?
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex trace_ -d "$OUT/pmc_$C" -o run --output-format csv -- \
       python3 bench.py --precision "$PREC" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/pmc_$C.log" 2>&1 || exit $?
@@ -38,3 +34,8 @@ json.dump(db, open(path, "w"), indent=1)
 json.dump(rec, open(f"{out}/traffic.json", "w"), indent=1)
 print(json.dumps(rec))
 EOF
+# bench line and kernel trace after the traffic passes, so bench.json reads this round's traffic
+timeout -k 10 300 python3 bench.py --precision "$PREC" --steps $STEPS > "$OUT/bench.log" 2>&1 || exit $?
+grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- \
+    python3 bench.py --precision "$PREC" --steps $STEPS --cpu-seconds 0 > "$OUT/ktrace.log" 2>&1 || exit $?
