@@ -85,6 +85,7 @@ template <typename T> struct KParams {
     uint32_t n_items;
     char* scratch;             // per-wave scratch regions
     size_t scratch_stride;
+    uint32_t vbytes, sbytes;   // trace_paths: value-array bytes, per-slot record bytes (PScratch)
 };
 
 constexpr int kSegShards = 256;
@@ -469,6 +470,262 @@ __global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
     }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Path regeneration.  Each ray of a pixel evolves independently of the others: bounce k of
+// sample s depends only on (origin, direction, colour, s, k).  The reference's positions are a
+// function of the termination bounces alone: with e_s = the bounce at which sample s hit the sky
+// (or depth if it was still enabled after the last bounce), the stable shuffle keeps sample
+// order, so at bounce k sample s sits at pos_k(s) = #{s' < s : e_s' >= k}, and a ray terminated
+// at bounce k moves to n_{k+1} + #{s' < s : e_s' == k}.  So each lane keeps ONE ray in registers
+// from its camera ray to its termination, then takes the next sample (of this pixel or of the
+// next pixel the wave pulls), and writes one record (e_s, colour, primary y) per sample.  When
+// all samples of a pixel are done, the wave replays the positions from the records, applies the
+// retire rule and sums in the reference's order — the same values, bit for bit,
+// as the bounce-synchronous schedule, with every lane busy and no per-bounce ray-state traffic.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kSlots = 8;   // pixels a wave may have in flight (lane s holds slot s's metadata)
+
+// Per-wave scratch of trace_paths: the position-indexed value array (3 x P) for the pixel being
+// reduced, then kSlots record regions {y[P], c[3][P], e[P]} indexed by sample.
+template <typename T> struct PScratch {
+    char* base;        // wave-uniform
+    uint32_t P, vbytes, sbytes;
+    __device__ __forceinline__ T& v(uint32_t ch, uint32_t q) const {
+        return *(T*)(base + (ch * P + q) * (uint32_t)sizeof(T));
+    }
+    __device__ __forceinline__ T& y(uint32_t s, uint32_t i) const {
+        return *(T*)(base + vbytes + s * sbytes + i * (uint32_t)sizeof(T));
+    }
+    __device__ __forceinline__ T& c(uint32_t s, uint32_t ch, uint32_t i) const {
+        return *(T*)(base + vbytes + s * sbytes + ((1u + ch) * P + i) * (uint32_t)sizeof(T));
+    }
+    __device__ __forceinline__ uint32_t& e(uint32_t s, uint32_t i) const {
+        return *(uint32_t*)(base + vbytes + s * sbytes + 4u * P * (uint32_t)sizeof(T) + i * 4u);
+    }
+};
+__host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t tsz) { return (3u * P * tsz + 255u) & ~255u; }
+__host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz) { return (P * (4u * tsz + 4u) + 255u) & ~255u; }
+
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
+// pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
+template <typename T>
+__device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item,
+                                                          uint32_t* hist) {
+    const auto& q = *cold_args<T>();
+    const uint32_t lane = threadIdx.x & 63u;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
+    // Value init: positions [spp, P) are the missing lanes of a partial last chunk, disabled from
+    // the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424) with a zero
+    // primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel == 0).
+    // Positions [0, spp) start at 0 (a ray still enabled at the end contributes black).
+    {
+        const V3<T> s0 = sky(T(0.0));
+        const bool white0 = q.s_sel == 0u;
+        for (uint32_t qi = lane; qi < P; qi += 64u) {
+            T vr = 0, vg = 0, vb = 0;
+            if (qi >= spp) {
+                if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
+                else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
+            }
+            sc.v(0, qi) = vr; sc.v(1, qi) = vg; sc.v(2, qi) = vb;
+        }
+    }
+    // Bounce iterations the reference runs: K = min(depth, max e + 1).
+    uint32_t K = 0;
+    if (depth > 0) {
+        uint32_t me = 0;
+        for (uint32_t i = lane; i < spp; i += 64u) me = max(me, sc.e(s, i));
+        K = min(depth, __builtin_amdgcn_readfirstlane(wave_max(me)) + 1u);
+    }
+    wave_mem_sync();
+    uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
+    for (uint32_t k = 0; k < K; ++k) {
+        if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
+            kb = k;
+            hist[lane] = 0;
+            __builtin_amdgcn_wave_barrier();
+            for (uint32_t i = lane; i < spp; i += 64u) {
+                const uint32_t e = sc.e(s, i);
+                if (e >= kb && e - kb < 64u) atomicAdd(&hist[e - kb], 1u);
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+        }
+        const uint32_t m = __builtin_amdgcn_readfirstlane(hist[k - kb]);   // rays hitting the sky at k
+        const uint32_t n_next = n - m;
+        const uint32_t Lnext = (k + 1 == depth) ? 0u : (n_next + 3u) / 4u;
+        if (m > 0) {
+            const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;   // positions retiring at bounce k
+            const bool U = q.s_sel == (k & 1u);                 // final read = this bounce's unsorted buffer
+            uint32_t cge = 0, ceq = 0;
+            for (uint32_t b = 0; b < spp && ceq < m; b += 64u) {
+                const uint32_t i = b + lane;
+                const uint32_t e = i < spp ? sc.e(s, i) : 0xFFFFFFFFu;
+                const bool ge = i < spp && e >= k, eq = e == k;
+                const unsigned long long bge = __ballot(ge), beq = __ballot(eq);
+                if (eq) {
+                    const uint32_t pold = cge + (uint32_t)__popcll(bge & lt_mask);
+                    const uint32_t pnew = n_next + ceq + (uint32_t)__popcll(beq & lt_mask);
+                    const V3<T> c = mk(sc.c(s, 0, i), sc.c(s, 1, i), sc.c(s, 2, i));
+                    if (U && pold >= lo && pold < hi) {
+                        const V3<T> sk = sky(sc.y(s, pold));
+                        sc.v(0, pold) = c.x * sk.x; sc.v(1, pold) = c.y * sk.y; sc.v(2, pold) = c.z * sk.z;
+                    }
+                    if (!U || pnew < lo || pnew >= hi) {
+                        const V3<T> sk = sky(sc.y(s, pnew));
+                        sc.v(0, pnew) = c.x * sk.x; sc.v(1, pnew) = c.y * sk.y; sc.v(2, pnew) = c.z * sk.z;
+                    }
+                }
+                cge += (uint32_t)__popcll(bge);
+                ceq += (uint32_t)__popcll(beq);
+            }
+        }
+        n = n_next;
+        Lcur = Lnext;
+    }
+    wave_mem_sync();
+    // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
+    // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
+    T acc = T(0.0);
+    if (lane < 12u) {
+        const uint32_t ch = lane >> 2, l = lane & 3u;
+        uint32_t j = 0;
+        for (; j + 16 <= C; j += 16) {
+            T v[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u) v[u] = sc.v(ch, 4 * (j + u) + l);
+#pragma unroll
+            for (int u = 0; u < 16; ++u) acc = acc + v[u];
+        }
+        for (; j < C; ++j) acc = acc + sc.v(ch, 4 * j + l);
+    }
+    const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
+            s3 = __shfl(acc, (int)((lane + 3) & 63u));
+    if (lane < 12u && (lane & 3u) == 0u) {
+        const uint32_t ch = lane >> 2;
+        const T tot = (((T(0.0) + acc) + s1) + s2) + s3;
+        const T v = tot / (T)spp;                                   // renderer.rs:161
+        if (!(v <= T(2.0))) atomicOr(q.err, 1u);                    // color.rs:55-57 assert
+        if (q.rgb) q.rgb[(size_t)item * 3 + ch] = q8(v);
+        if (q.lin) q.lin[(size_t)item * 3 + ch] = (double)v;
+    }
+    return K;
+}
+
+// Persistent path-regeneration kernel (see above).  Wave-uniform state: the slot being issued
+// (cur, next sample cur_next), the busy-slot mask, and per-slot pixel/remaining-sample counts held
+// in lane s of two VGPRs.  Per iteration: hand free lanes new samples, trace one bounce for every
+// live ray (one sphere sweep for the whole wave), record terminations, finish completed pixels.
+template <typename T, int W, bool ROOT2>
+__global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
+    __shared__ unsigned long long wcount[4][3];
+    __shared__ uint32_t s_hist[4][64];
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    PScratch<T> sc;
+    uint32_t spp, depth, n_items;
+    {
+        const auto& q = *cold_args<T>();
+        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+        sc = PScratch<T>{q.scratch + (size_t)gw * q.scratch_stride, q.P, q.vbytes, q.sbytes};
+        spp = q.spp; depth = q.depth; n_items = q.n_items;
+    }
+    V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
+    uint32_t sid = 0, k = 0, slot = 0, pix = 0;
+    bool live = false;
+    uint32_t slot_item = 0, slot_left = 0;   // lane s < kSlots: pixel item and unfinished samples of slot s
+    uint32_t busy = 0, cur = 0, cur_next = spp, cur_pix = 0, cur_row = 0, cur_col = 0;
+    bool drained = false;
+    for (;;) {
+        // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
+        bool fresh = false;
+        uint32_t frow = 0, fcol = 0;
+        unsigned long long freem = __ballot(!live);
+        while (freem != 0ull && !drained) {
+            if (cur_next == spp) {
+                const uint32_t avail = ~busy & ((1u << kSlots) - 1u);
+                if (avail == 0u) break;   // every slot waits for straggler rays
+                const auto& q = *cold_args<T>();
+                uint32_t item = 0;
+                if (lane == 0) item = atomicAdd(q.counter, 1u);
+                item = __builtin_amdgcn_readfirstlane(item);
+                if (item >= n_items) { drained = true; break; }
+                const uint32_t s = __builtin_ctz(avail);
+                const uint32_t ri = item / q.col_count, ci = item % q.col_count;
+                cur_row = q.row_begin + ri * q.row_step;
+                cur_col = q.col_begin + ci;
+                cur_pix = cur_row * q.W + cur_col;
+                if (lane == s) { slot_item = item; slot_left = spp; }
+                busy |= 1u << s;
+                cur = s;
+                cur_next = 0;
+            }
+            const bool isfree = (freem >> lane) & 1ull;
+            const uint32_t take = min((uint32_t)__popcll(freem), spp - cur_next);
+            const uint32_t r = (uint32_t)__popcll(freem & lt_mask);
+            const bool mine = isfree && r < take;
+            if (mine) { fresh = true; sid = cur_next + r; slot = cur; pix = cur_pix; frow = cur_row; fcol = cur_col; }
+            freem &= ~__ballot(mine);
+            cur_next += take;
+        }
+        if (fresh) {   // Camera::get_ray (ray_tracing.rs:77-89); primary y kept for quirk Q2
+            camera_ray(p, fcol, frow, pix, sid, o, d);
+            c = mk(T(1.0), T(1.0), T(1.0));
+            k = 0;
+            live = true;
+            sc.y(slot, sid) = d.y;
+        }
+        if (__ballot(live) == 0ull) break;   // drained, and every slot finished
+        // ---- one bounce for every live ray ----
+        const bool act = live && k < depth;
+        bool surv = false;
+        if (act) surv = bounce<T, ROOT2>(p, o, d, c, pix, sid, k);
+        const unsigned long long bact = __ballot(act);
+        if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
+        // ---- terminations: record e (and the colour of a sky hit) ----
+        const bool term = live && (!act || !surv || k + 1 == depth);
+        if (term) {
+            const bool skyhit = act && !surv;
+            sc.e(slot, sid) = skyhit ? k : depth;
+            if (skyhit) { sc.c(slot, 0, sid) = c.x; sc.c(slot, 1, sid) = c.y; sc.c(slot, 2, sid) = c.z; }
+        }
+        if (act && surv) k += 1u;
+        live = live && !term;
+        unsigned long long tm = __ballot(term);
+        bool synced = false;
+        while (tm != 0ull) {
+            const uint32_t s = __builtin_amdgcn_readlane(slot, __builtin_ctzll(tm));
+            const unsigned long long m = __ballot(term && slot == s);
+            tm &= ~m;
+            if (lane == s) slot_left -= (uint32_t)__popcll(m);
+            if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
+                if (!synced) { wave_mem_sync(); synced = true; }
+                const uint32_t K = finish_pixel<T>(sc, s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
+                if (lane == 0) wcount[wave][2] += K;
+                busy &= ~(1u << s);
+            }
+        }
+    }
+    if (lane == 0) {
+        const auto& q = *cold_args<T>();
+        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+        unsigned long long* cc = &q.segs[(gw & (kSegShards - 1)) * kSegStride];
+        atomicAdd(cc + 0, wcount[wave][0]);
+        atomicAdd(cc + 1, wcount[wave][1]);
+        atomicAdd(cc + 2, wcount[wave][2]);
+    }
+}
+
 }  // namespace rt
 
 // ============================== host side ==============================
@@ -712,7 +969,11 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
     const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
-    void (*kern)(KParams<T>) =
+    static const bool use_waves = [] { const char* e = getenv("RT_KERNEL"); return e && !strcmp(e, "waves"); }();
+    void (*kern)(KParams<T>) = !use_waves ?
+        (r2 ? trace_paths<T, kWavesRoot2, true>
+           : (W >= 8 ? trace_paths<T, 8, false> : W >= 6 ? trace_paths<T, 6, false> : W >= 5 ? trace_paths<T, 5, false>
+            : W >= 4 ? trace_paths<T, 4, false> : trace_paths<T, 1, false>)) :
         r2 ? trace_waves<T, kWavesRoot2, true>
            : (W >= 8 ? trace_waves<T, 8, false> : W >= 6 ? trace_waves<T, 6, false> : W >= 5 ? trace_waves<T, 5, false>
             : W >= 4 ? trace_waves<T, 4, false> : trace_waves<T, 1, false>);
@@ -722,7 +983,13 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
     const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
     if (nblocks > need) nblocks = need;
-    p.scratch_stride = scratch_bytes(p.P, sizeof(T));
+    p.vbytes = paths_vbytes(p.P, sizeof(T));
+    p.sbytes = paths_sbytes(p.P, sizeof(T));
+    p.scratch_stride = use_waves ? scratch_bytes(p.P, sizeof(T)) : (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
+    // Keep the scratch within a fixed budget: fewer resident waves for very large spp.
+    const uint64_t kScratchBudget = 24ull << 30;
+    const uint64_t max_blocks = kScratchBudget / (4 * p.scratch_stride);
+    if (nblocks > max_blocks) nblocks = max_blocks > 0 ? max_blocks : 1;
     const int rc = ensure_scratch(c, p.scratch_stride * nblocks * 4, st);
     if (rc != RT_OK) return rc;
     p.scratch = (char*)c->scratch;
