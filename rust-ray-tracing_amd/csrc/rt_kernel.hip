@@ -42,6 +42,10 @@ namespace rt {
 template <typename T> struct MatT {
     uint32_t kind, hollow;
     T ar, ag, ab, fuzz, ior;
+    // Dielectric constants precomputed on the host in T with the reference's operations (IEEE,
+    // no contraction, so the bits equal the per-ray device computation): 1/ior (materials.rs:131)
+    // and Schlick's r0 = ((1-ratio)/(1+ratio))^2 (materials.rs:122) for ratio = 1/ior and ior.
+    T inv_ior, r0_front, r0_back;
 };
 
 // Device sphere layout (rt_context_set_scene): 64-byte groups, one s_load_dwordx16 each, padded
@@ -94,6 +98,18 @@ constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured s
 constexpr int kWavesF64 = 5;
 constexpr int kWavesRoot2 = 6;  // the Q1-off (scalar semantics) variant
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
+
+// Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..6.
+#ifdef RT_KSTATS
+__shared__ unsigned long long g_kst[4][4];
+__device__ __forceinline__ void kstat(uint32_t i, uint32_t n = 1) {
+    const unsigned long long ex = __builtin_amdgcn_read_exec();
+    if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex)) atomicAdd(&g_kst[threadIdx.x >> 6][i], (unsigned long long)n);
+}
+#define KSTAT(...) kstat(__VA_ARGS__)
+#else
+#define KSTAT(...) ((void)0)
+#endif
 
 // Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
 // wave-uniform, so these become s_load into SGPRs — a free broadcast to all 64 lanes.
@@ -172,6 +188,7 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     // for a candidate whose discriminant is non-negative.  Exact pre-filter: with hb >= 0,
     // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
     auto hit = [&](T hb, T disc, uint32_t i) {
+        KSTAT(1);
         const T sd = sqrt(disc);
         const T r1 = (-hb - sd) * inv_a;                       // :270
         bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
@@ -187,11 +204,21 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
     cptr<T> f = (cptr<T>)__builtin_assume_aligned(p.sph, 64);
     const uint32_t ng = p.n_groups;
-    // Candidate filter, branch-free: m = min(disc, -hb) >= 0 holds whenever disc >= 0 && hb < 0
-    // (the only case in which root1 can be valid); its false positives (hb == 0, NaN) are
-    // rejected again inside hit(), so the filter never changes a result.  One wave-level branch
-    // per 64-byte group keeps the scalar unit (shared by the CU's 4 SIMDs) off the critical path.
-    auto cand = [&](T hb, T disc) -> T { return root2 ? disc : fmin(disc, -hb); };
+    // Candidate filter, branch-free, on sign bits: cand(hb, disc) = ~bits(disc) & bits(hb) has its
+    // sign bit set iff disc >= +0 and hb <= -0 — the only case in which root1 = (-hb - sqrt(disc))
+    // * inv_a can be valid (root1 > 0 needs -hb > 0; NaNs never give a valid root).  disc is never
+    // -0: fma(hb, hb, -(a*c)) rounds an exact zero to +0.  hb == -0 and disc == +inf pass and are
+    // rejected again inside hit(), so the filter never changes a result.  Four v_bitop3 + one
+    // compare per 64-byte group, one wave-level branch per group.  Q1-off (root2) needs disc >= 0 only.
+    auto sbits = [](T x) -> uint32_t {
+        if constexpr (sizeof(T) == 4) return __float_as_uint(x);
+        else return (uint32_t)__double2hiint(x);
+    };
+    auto cand = [&](T hb, T disc) -> uint32_t { return root2 ? ~sbits(disc) : (~sbits(disc) & sbits(hb)); };
+    auto is_cand = [](uint32_t m) -> bool { return (int32_t)m < 0; };
+    // Per-sphere test inside a taken group: a float superset of cand (hb == +0 passes too), so the
+    // group test can fold the four sign words into one chain of v_bitop3.
+    auto cand_f = [&](T hb, T disc) -> bool { return root2 ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)); };
     if constexpr (sizeof(T) == 4) {
         // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two spheres,
         // so the results are bit-identical to the scalar sequence (:252-257).
@@ -209,14 +236,25 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
                 const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;      // :256
                 disc[q] = fma2(hb[q], hb[q], na * c);                             // :257
             }
-            const T m0 = cand(hb[0].x, disc[0].x), m1 = cand(hb[0].y, disc[0].y);
-            const T m2 = cand(hb[1].x, disc[1].x), m3 = cand(hb[1].y, disc[1].y);
-            if (fmax(fmax(m0, m1), fmax(m2, m3)) >= T(0.0)) {
+            // acc = cand0 | cand1 | cand2 | cand3 as a strict chain: v_bitop3 computes
+            // S0 | (~S1 & S2) (table 0xF2) in one op, so the group test is 4 VALU + 1 compare.
+            uint32_t acc = cand(hb[0].x, disc[0].x);
+            if constexpr (!root2) {
+                acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[0].y), sbits(hb[0].y), 0xF2);
+                acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[1].x), sbits(hb[1].x), 0xF2);
+                acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[1].y), sbits(hb[1].y), 0xF2);
+            } else {
+                acc = acc | cand(hb[0].y, disc[0].y) | cand(hb[1].x, disc[1].x) | cand(hb[1].y, disc[1].y);
+            }
+            if (is_cand(acc)) {
+                KSTAT(0);
+                KSTAT(2, (uint32_t)__popcll(__ballot(cand_f(hb[0].x, disc[0].x))) + (uint32_t)__popcll(__ballot(cand_f(hb[0].y, disc[0].y))) +
+                         (uint32_t)__popcll(__ballot(cand_f(hb[1].x, disc[1].x))) + (uint32_t)__popcll(__ballot(cand_f(hb[1].y, disc[1].y))));
                 const uint32_t i0 = 4 * g;
-                if (m0 >= T(0.0)) hit(hb[0].x, disc[0].x, i0);
-                if (m1 >= T(0.0)) hit(hb[0].y, disc[0].y, i0 + 1);
-                if (m2 >= T(0.0)) hit(hb[1].x, disc[1].x, i0 + 2);
-                if (m3 >= T(0.0)) hit(hb[1].y, disc[1].y, i0 + 3);
+                if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, i0);
+                if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, i0 + 1);
+                if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, i0 + 2);
+                if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, i0 + 3);
             }
         };
         sphere_loop(f, ng, group);
@@ -231,10 +269,10 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
                 const T c = pk_len2(oc) - v[3];                            // :256
                 disc[j] = fma(hb[j], hb[j], -a * c);                       // :257
             }
-            const T m0 = cand(hb[0], disc[0]), m1 = cand(hb[1], disc[1]);
-            if (fmax(m0, m1) >= T(0.0)) {
-                if (m0 >= T(0.0)) hit(hb[0], disc[0], 2 * g);
-                if (m1 >= T(0.0)) hit(hb[1], disc[1], 2 * g + 1);
+            const uint32_t m0 = cand(hb[0], disc[0]), m1 = cand(hb[1], disc[1]);
+            if (is_cand(m0 | m1)) {
+                if (cand_f(hb[0], disc[0])) hit(hb[0], disc[0], 2 * g);
+                if (cand_f(hb[1], disc[1])) hit(hb[1], disc[1], 2 * g + 1);
             }
         };
         sphere_loop(f, ng, group);
@@ -254,22 +292,24 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     const MatT<T> m = q.mats[q.smat[best]];
     const U4 r = philox(sid, pix, k, 2u, q.k0, q.k1);
     V3<T> nd;
-    if (m.kind == RT_LAMBERTIAN) {
-        nd = add(unit_vec(u01a(r, T(0)), u01b(r, T(0))), nrm);
-        if (near_zero(nd)) nd = nrm;
-        col = mk(col.x * m.ar, col.y * m.ag, col.z * m.ab);
-    } else if (m.kind == RT_METAL) {
-        nd = add(reflect(d, nrm), mul(unit_vec(u01a(r, T(0)), u01b(r, T(0))), m.fuzz));
+    if (m.kind != RT_DIELECTRIC) {
+        // One random_unit_vector for both kinds (a wave usually holds both: one evaluation, not two).
+        const V3<T> rv = unit_vec(u01a(r, T(0)), u01b(r, T(0)));
+        if (m.kind == RT_LAMBERTIAN) {
+            nd = add(rv, nrm);
+            if (near_zero(nd)) nd = nrm;
+        } else {
+            nd = add(reflect(d, nrm), mul(rv, m.fuzz));
+        }
         col = mk(col.x * m.ar, col.y * m.ag, col.z * m.ab);
     } else {
-        const T ratio = front ? T(1.0) / m.ior : m.ior;
+        const T ratio = front ? m.inv_ior : m.ior;
         const V3<T> nn = m.hollow ? neg(nrm) : nrm;
         const T ct = fmin(dot(neg(d), nn), T(1.0));
         const T st = sqrt(T(1.0) - ct * ct);
         bool refl = ratio * st > T(1.0);
         if (!refl) {   // Dielectric::reflectance (materials.rs:121-124), powi(5) = x*((x*x)*(x*x))
-            const T q = (T(1.0) - ratio) / (T(1.0) + ratio);
-            const T r0 = q * q;
+            const T r0 = front ? m.r0_front : m.r0_back;
             const T m1 = T(1.0) - ct;
             const T m2 = m1 * m1;
             const T m5 = m1 * (m2 * m2);
@@ -631,6 +671,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
+#ifdef RT_KSTATS
+    if (lane < 4) g_kst[wave][lane] = 0;
+#endif
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     PScratch<T> sc;
     uint32_t spp, depth, n_items;
@@ -678,6 +721,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             freem &= ~__ballot(mine);
             cur_next += take;
         }
+        KSTAT(3, __ballot(fresh) != 0ull ? 1u : 0u);
         if (fresh) {   // Camera::get_ray (ray_tracing.rs:77-89); primary y kept for quirk Q2
             camera_ray(p, fcol, frow, pix, sid, o, d);
             c = mk(T(1.0), T(1.0), T(1.0));
@@ -723,6 +767,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         atomicAdd(cc + 0, wcount[wave][0]);
         atomicAdd(cc + 1, wcount[wave][1]);
         atomicAdd(cc + 2, wcount[wave][2]);
+#ifdef RT_KSTATS
+        for (int i = 0; i < 4; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);
+#endif
     }
 }
 
@@ -874,7 +921,11 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
     mats.resize(s->n_materials ? s->n_materials : 1);
     for (uint32_t i = 0; i < s->n_materials; ++i) {
         const rt_material& m = s->materials[i];
-        mats[i] = MatT<T>{m.kind, m.hollow, (T)m.albedo[0], (T)m.albedo[1], (T)m.albedo[2], (T)m.fuzz, (T)m.ior};
+        const T ior = (T)m.ior, one = T(1.0);
+        const T inv = one / ior;
+        const T qf = (one - inv) / (one + inv), qb = (one - ior) / (one + ior);
+        mats[i] = MatT<T>{m.kind, m.hollow, (T)m.albedo[0], (T)m.albedo[1], (T)m.albedo[2], (T)m.fuzz, ior,
+                          inv, qf * qf, qb * qb};
     }
 }
 
@@ -1050,7 +1101,12 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
     HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
     HIPCHK(hipMemset(c->err, 0, 16));
-    uint64_t total = 0, slots = 0, iters = 0;
+    uint64_t total = 0, slots = 0, iters = 0, kst[4] = {0, 0, 0, 0};
+    for (int i = 0; i < kSegShards; ++i)
+        for (int j = 0; j < 4; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
+    if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
+        fprintf(stderr, "rt_kstats: taken_groups %llu hit_branches %llu hit_lanes %llu camera_iters %llu\n",
+                (unsigned long long)kst[0], (unsigned long long)kst[1], (unsigned long long)kst[2], (unsigned long long)kst[3]);
     for (int i = 0; i < kSegShards; ++i) {
         total += segs[(size_t)i * kSegStride];
         slots += segs[(size_t)i * kSegStride + 1];

@@ -63,7 +63,7 @@ class RtStats(ctypes.Structure):
 
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "librt_mi355x.so")
+LIB_PATH = os.environ.get("RT_MI355X_LIB") or os.path.join(PKG_DIR, "lib", "librt_mi355x.so")
 
 # Every symbol include/rt_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED = [

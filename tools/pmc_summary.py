@@ -9,7 +9,7 @@ d = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 tot, dispatches = {}, set()
 for f in sorted(glob.glob(f"{d}/pass*/*counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        if "trace_waves" not in r["Kernel_Name"]:
+        if "trace_" not in r["Kernel_Name"]:
             continue
         dispatches.add((f, r["Dispatch_Id"]))
         tot[r["Counter_Name"]] = tot.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
