@@ -31,7 +31,7 @@ extern "C" {
 #define RT_ERR_HIP 2         /* HIP runtime failure (no device, launch failure, OOM) */
 #define RT_ERR_RANGE 3       /* a pixel channel exceeded 2.0 after /spp: the reference panics in
                                 Color::to_u8_array (color.rs:55-57); the image is still written */
-#define RT_ERR_UNSUPPORTED 4 /* configuration this build cannot run (e.g. spp beyond the LDS budget) */
+#define RT_ERR_UNSUPPORTED 4 /* configuration this build cannot run (e.g. spp > 2^20) */
 
 /* ---- materials (src/materials.rs:41-155) ---- */
 #define RT_LAMBERTIAN 0u
@@ -93,6 +93,17 @@ typedef struct rt_stats {
 #define RT_FLAG_F32 0x1u     /* compute in fp32 (default: fp64, the reference's arithmetic) */
 #define RT_FLAG_ROOT2 0x2u   /* quirk Q1 off: accept the far root like scalar Sphere::hit
                                 (objects.rs:228-234) instead of testing root1 twice (objects.rs:273) */
+/* Semantics modes (at most one; default = the live path, TileRenderTask::render_vectorized2 ->
+ * Scene::trace_vectorized2, renderer.rs:141-176, quirks Q1-Q3 as the reference has them):
+ *   RT_FLAG_MODE_VECTORIZED: render_vectorized -> Scene::trace_vectorized (renderer.rs:102-139,
+ *     ray_tracing.rs:312-373): each sample keeps its own value and the sky uses its own final
+ *     direction (Q2, Q3 off); hit_packed is shared, so Q1 still applies unless RT_FLAG_ROOT2.
+ *   RT_FLAG_MODE_SCALAR: TileRenderTask::render -> Scene::trace_rays (renderer.rs:68-100,
+ *     ray_tracing.rs:264-306): scalar Sphere::hit (objects.rs:216-247; no FMA, both roots, normal
+ *     divided by the signed radius), the first of equal hits wins (min_by_key), Color::average. */
+#define RT_FLAG_MODE_VECTORIZED 0x4u
+#define RT_FLAG_MODE_SCALAR 0x8u
+#define RT_FLAG_ALL 0xFu      /* any other bit is RT_ERR_INVALID */
 
 /* Camera::new (ray_tracing.rs:27-62).  view_angle and defocus_angle in degrees. */
 int rt_camera_new(rt_camera* out, uint32_t image_width, uint32_t image_height, double focal_length,

@@ -54,13 +54,22 @@ typedef struct or_camera {
 
 /* flag bits (same values as RT_FLAG_* in include/rt_mi355x.h) */
 #define OR_FLAG_ROOT2 0x2u   /* Q1 off: accept root2 like scalar Sphere::hit (objects.rs:228-234) */
+/* Semantics modes (default: trace_vectorized2 via render_vectorized2, renderer.rs:141-176):
+ *   VECTORIZED: trace_vectorized (ray_tracing.rs:312-373) via render_vectorized (renderer.rs:102-139)
+ *               — per-chunk, final-ray sky (Q2 off), every ray keeps its own value (Q3 off);
+ *               hit_packed is shared with the default mode, so Q1 / OR_FLAG_ROOT2 still apply.
+ *   SCALAR:     trace_rays (ray_tracing.rs:264-306) via render (renderer.rs:68-100) — scalar
+ *               Sphere::hit (objects.rs:216-247: both roots, no FMA, normal / signed radius),
+ *               first minimum wins ties, Color::average in sample order. */
+#define OR_FLAG_MODE_VECTORIZED 0x4u
+#define OR_FLAG_MODE_SCALAR 0x8u
 
 /* Render the listed pixels (global index row*W+col; NULL = all W*H in order).
  * rgb_out: n*3 bytes, lin_out: n*3 doubles (pixel colour after /spp, before
  * gamma), either may be NULL.  *segments (may be NULL) receives the number of
  * enabled rays traced (sum over bounces of enabled lanes).
  * Returns 0, or 3 if some channel exceeded 2.0 (the reference panics there,
- * color.rs:55-57), or 1 on bad arguments. */
+ * color.rs:55-57), or 1 on bad arguments (including both mode bits set). */
 int oracle_render_f64(const or_scene* sc, const or_camera* cam, uint32_t max_bounces,
                       uint32_t spp, uint64_t seed, uint32_t flags,
                       const uint32_t* pixels, uint32_t n_pixels,

@@ -415,6 +415,109 @@ static void SFX(trace_pixel)(const SFX(scene_r)* S, SFX(ws)* w, uint32_t depth, 
     *segs += nseg;
 }
 
+/* ---- "vectorized" mode: Scene::trace_vectorized, ray_tracing.rs:312-373 (one PackedRays<4>
+ * chunk, no shuffle), as called by render_vectorized (renderer.rs:102-139). ---- */
+static void SFX(trace_chunk_v1)(const SFX(scene_r)* S, SFX(prays) R, uint32_t depth, uint32_t pix,
+                                uint32_t k0, uint32_t k1, uint32_t flags, SFX(pcol)* out, uint64_t* segs) {
+    SFX(pcol) col;
+    int sky[4] = {0, 0, 0, 0};
+    for (int l = 0; l < 4; ++l) {                                                      /* :319-320 */
+        REAL w = R.en[l] ? (REAL)1.0 : (REAL)0.0;
+        col.r[l] = w; col.g[l] = w; col.b[l] = w;
+    }
+    for (uint32_t k = 0; k < depth; ++k) {                                            /* :323 */
+        if (!(R.en[0] | R.en[1] | R.en[2] | R.en[3])) break;                          /* :324-327 */
+        SFX(phit) H;
+        for (int l = 0; l < 4; ++l) {
+            H.t[l] = (REAL)INFINITY; H.hit[l] = 0; H.front[l] = 0; H.mat[l] = 0;
+            H.nx[l] = H.ny[l] = H.nz[l] = 0;
+            *segs += (uint64_t)R.en[l];
+        }
+        for (uint32_t i = 0; i < S->n; ++i)                                          /* :331-333 */
+            SFX(hit_packed)(&R, S->cx[i], S->cy[i], S->cz[i], S->r[i], S->mat[i], &H, flags);
+        SFX(finalize)(&R, &H);                                                        /* :335 */
+        for (int l = 0; l < 4; ++l) {                                                 /* :339-360 */
+            if (H.hit[l]) {
+                V3 d = SFX(mk)(R.dx[l], R.dy[l], R.dz[l]);
+                V3 p = SFX(mk)(H.px[l], H.py[l], H.pz[l]);
+                V3 n = SFX(mk)(H.nx[l], H.ny[l], H.nz[l]);
+                V3 nd;
+                REAL att[3];
+                SFX(scatter)(&S->mats[H.mat[l]], d, p, n, H.front[l], pix, R.sid[l], k, k0, k1, &nd, att);
+                col.r[l] = col.r[l] * att[0]; col.g[l] = col.g[l] * att[1]; col.b[l] = col.b[l] * att[2];
+                R.ox[l] = p.x; R.oy[l] = p.y; R.oz[l] = p.z;
+                R.dx[l] = nd.x; R.dy[l] = nd.y; R.dz[l] = nd.z;
+            } else {                                                                  /* :355-358 */
+                R.en[l] = 0;
+                sky[l] = 1;
+            }
+        }
+    }
+    for (int l = 0; l < 4; ++l) {   /* :365-370: sky from the FINAL direction of each lane */
+        REAL sk[3];
+        SFX(sky)(R.dy[l], sk);
+        REAL cr = col.r[l], cg = col.g[l], cb = col.b[l];
+        if (sky[l]) { cr = cr * sk[0]; cg = cg * sk[1]; cb = cb * sk[2]; }
+        if (R.en[l]) { cr = 0; cg = 0; cb = 0; }
+        out->r[l] = cr; out->g[l] = cg; out->b[l] = cb;
+    }
+}
+
+/* ---- "scalar" mode: Sphere::hit (objects.rs:216-247), Scene::hit (ray_tracing.rs:231-235),
+ * Scene::trace_rays (ray_tracing.rs:264-306) as called by TileRenderTask::render
+ * (renderer.rs:68-100).  Scalar Vec3 arithmetic (no FMA), both roots, true division by a,
+ * normal divided by the signed radius, the first minimum wins ties (min_by_key). ---- */
+static int SFX(scene_hit_scalar)(const SFX(scene_r)* S, V3 o, V3 d, REAL* t_out, uint32_t* i_out) {
+    int found = 0;
+    REAL best = 0;
+    for (uint32_t i = 0; i < S->n; ++i) {
+        V3 oc = SFX(sub)(o, SFX(mk)(S->cx[i], S->cy[i], S->cz[i]));                   /* :217 */
+        REAL a = SFX(len2)(d);                                                         /* :219 */
+        REAL hb = SFX(dot)(oc, d);                                                     /* :220 */
+        REAL c = SFX(len2)(oc) - S->r[i] * S->r[i];                                    /* :221 */
+        REAL disc = hb * hb - a * c;                                                   /* :222 */
+        if (disc < (REAL)0.0) continue;                                                /* :223-225 */
+        REAL sd = SQRT(disc);
+        REAL root = (-hb - sd) / a;                                                    /* :228 */
+        if (!(root >= (REAL)0.001 && root < (REAL)INFINITY)) {                         /* :229-234 */
+            root = (-hb + sd) / a;
+            if (!(root >= (REAL)0.001 && root < (REAL)INFINITY)) continue;
+        }
+        if (!found || root < best) { best = root; *i_out = i; found = 1; }            /* min_by_key: first min */
+    }
+    *t_out = best;
+    return found;
+}
+
+static void SFX(trace_ray_scalar)(const SFX(scene_r)* S, V3 o, V3 d, uint32_t depth, uint32_t pix, uint32_t sid,
+                                  uint32_t k0, uint32_t k1, REAL out[3], uint64_t* segs) {
+    REAL cr = 1, cg = 1, cb = 1;                                                       /* :266-269 */
+    int alive = 1;
+    for (uint32_t k = 0; k < depth && alive; ++k) {                                   /* :272-302 */
+        *segs += 1;
+        REAL t;
+        uint32_t i;
+        if (SFX(scene_hit_scalar)(S, o, d, &t, &i)) {
+            V3 p = SFX(add)(o, SFX(mul)(d, t));                                        /* Ray::at, ray.rs:28-30 */
+            V3 outw = SFX(dvs)(SFX(sub)(p, SFX(mk)(S->cx[i], S->cy[i], S->cz[i])), S->r[i]);   /* objects.rs:242 */
+            int front = SFX(dot)(d, outw) < (REAL)0.0;                                /* HitRecord::new, objects.rs:69-73 */
+            V3 n = front ? outw : SFX(neg)(outw);
+            V3 nd;
+            REAL att[3];
+            SFX(scatter)(&S->mats[S->mat[i]], d, p, n, front, pix, sid, k, k0, k1, &nd, att);
+            cr = cr * att[0]; cg = cg * att[1]; cb = cb * att[2];                      /* :280 */
+            o = p; d = nd;
+        } else {                                                                       /* :283-292 */
+            REAL sk[3];
+            SFX(sky)(d.y, sk);   /* 0.5*(y+1), (1-a)+a*k: the same values as the packed gradient */
+            cr = cr * sk[0]; cg = cg * sk[1]; cb = cb * sk[2];
+            alive = 0;
+        }
+    }
+    if (alive) { cr = 0; cg = 0; cb = 0; }                                             /* :300-305 */
+    out[0] = cr; out[1] = cg; out[2] = cb;
+}
+
 /* Color::to_u8_array (color.rs:54-64): sqrt gamma, *255.999, saturating `as u8`, NaN -> 0. */
 static inline uint8_t SFX(q8)(REAL v) {
     REAL x = SQRT(v) * (REAL)255.999;
@@ -470,7 +573,33 @@ static void* SFX(worker)(void* arg) {
                 }
             }
             REAL sum[3];
-            SFX(trace_pixel)(J->S, &w, J->depth, pix, J->k0, J->k1, J->flags, sum, &segs);
+            if (J->flags & OR_FLAG_MODE_SCALAR) {
+                /* render (renderer.rs:80-86): trace_rays then Color::average, summed in sample order */
+                REAL acc[3] = {0, 0, 0};
+                for (uint32_t s = 0; s < J->spp; ++s) {
+                    const SFX(prays)* P = &w.rays0[s / 4u];
+                    const int l = (int)(s % 4u);
+                    REAL v[3];
+                    SFX(trace_ray_scalar)(J->S, SFX(mk)(P->ox[l], P->oy[l], P->oz[l]), SFX(mk)(P->dx[l], P->dy[l], P->dz[l]),
+                                          J->depth, pix, s, J->k0, J->k1, v, &segs);
+                    acc[0] = acc[0] + v[0]; acc[1] = acc[1] + v[1]; acc[2] = acc[2] + v[2];   /* color.rs:74-79 */
+                }
+                sum[0] = acc[0]; sum[1] = acc[1]; sum[2] = acc[2];
+            } else if (J->flags & OR_FLAG_MODE_VECTORIZED) {
+                /* render_vectorized (renderer.rs:116-124): per-lane sum over chunks, then PackedColor::sum */
+                REAL acc[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+                for (uint32_t j = 0; j < C; ++j) {
+                    SFX(pcol) pc;
+                    SFX(trace_chunk_v1)(J->S, w.rays0[j], J->depth, pix, J->k0, J->k1, J->flags, &pc, &segs);
+                    for (int l = 0; l < 4; ++l) {
+                        acc[0][l] = acc[0][l] + pc.r[l]; acc[1][l] = acc[1][l] + pc.g[l]; acc[2][l] = acc[2][l] + pc.b[l];
+                    }
+                }
+                for (int ch = 0; ch < 3; ++ch)
+                    sum[ch] = (((REAL)0.0 + acc[ch][0]) + acc[ch][1] + acc[ch][2]) + acc[ch][3];
+            } else {
+                SFX(trace_pixel)(J->S, &w, J->depth, pix, J->k0, J->k1, J->flags, sum, &segs);
+            }
             for (int ch = 0; ch < 3; ++ch) {
                 REAL v = sum[ch] / (REAL)J->spp;                                      /* renderer.rs:161 */
                 if (!(v <= (REAL)2.0)) panic = 1;                                     /* color.rs:55-57 */
@@ -492,6 +621,7 @@ int SFX(oracle_render)(const or_scene* sc, const or_camera* cam, uint32_t max_bo
                        const uint32_t* pixels, uint32_t n_pixels,
                        uint8_t* rgb_out, double* lin_out, uint64_t* segments, int n_threads) {
     if (!sc || !cam || spp == 0 || cam->image_width == 0 || cam->image_height == 0) return 1;
+    if ((flags & OR_FLAG_MODE_VECTORIZED) && (flags & OR_FLAG_MODE_SCALAR)) return 1;
     if (sc->n_spheres && (!sc->center || !sc->radius || !sc->material || !sc->materials)) return 1;
     for (uint32_t i = 0; i < sc->n_spheres; ++i)
         if (sc->material[i] >= sc->n_materials) return 1;

@@ -177,11 +177,14 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
 
 // One bounce of one enabled ray: the object loop of trace_vectorized2 (ray_tracing.rs:399-403)
 // + the per-lane material step (:406-426).  Returns true if the ray hit (and was scattered).
-template <typename T, bool root2>
+// SCALAR selects Sphere::hit + Scene::hit + HitRecord::new (objects.rs:216-247, ray_tracing.rs:231-235,
+// objects.rs:65-83): no FMA, both roots, root = (-hb -/+ sd) / a, the first minimum wins ties, and
+// the normal is (p - c) / radius with the signed radius.  Otherwise hit_packed + PackedHitRecords.
+template <typename T, bool root2, bool SCALAR = false>
 __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, V3<T>& col, uint32_t pix,
                                        uint32_t sid, uint32_t k) {
-    const T a = pk_len2(d);          // objects.rs:253
-    const T inv_a = T(1.0) / a;      // objects.rs:254 (loop-invariant)
+    const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
+    const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254 (loop-invariant)
     T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
     int best = -1;
     // Sphere::hit_packed (objects.rs:249-290) + PackedHitRecords::update (objects.rs:140-155)
@@ -189,6 +192,16 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
     auto hit = [&](T hb, T disc, uint32_t i) {
         KSTAT(1);
+        if constexpr (SCALAR) {   // objects.rs:227-234 and min_by_key (first minimum)
+            const T sd = sqrt(disc);
+            T root = (-hb - sd) / a;
+            if (!(root >= T(0.001) && root < T(INFINITY))) {
+                root = (-hb + sd) / a;
+                if (!(root >= T(0.001) && root < T(INFINITY))) return;
+            }
+            if (root < best_t) { best_t = root; best = (int)i; }
+            return;
+        }
         const T sd = sqrt(disc);
         const T r1 = (-hb - sd) * inv_a;                       // :270
         bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
@@ -214,11 +227,12 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
         if constexpr (sizeof(T) == 4) return __float_as_uint(x);
         else return (uint32_t)__double2hiint(x);
     };
-    auto cand = [&](T hb, T disc) -> uint32_t { return root2 ? ~sbits(disc) : (~sbits(disc) & sbits(hb)); };
+    constexpr bool kDiscOnly = root2 || SCALAR;   // both roots possible: disc >= 0 is the only filter
+    auto cand = [&](T hb, T disc) -> uint32_t { return kDiscOnly ? ~sbits(disc) : (~sbits(disc) & sbits(hb)); };
     auto is_cand = [](uint32_t m) -> bool { return (int32_t)m < 0; };
     // Per-sphere test inside a taken group: a float superset of cand (hb == +0 passes too), so the
     // group test can fold the four sign words into one chain of v_bitop3.
-    auto cand_f = [&](T hb, T disc) -> bool { return root2 ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)); };
+    auto cand_f = [&](T hb, T disc) -> bool { return kDiscOnly ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)); };
     if constexpr (sizeof(T) == 4) {
         // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two spheres,
         // so the results are bit-identical to the scalar sequence (:252-257).
@@ -232,14 +246,20 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
                 const T* v = &cur.v[8 * q];
                 const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
                 const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
-                hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));                   // :255
-                const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;      // :256
-                disc[q] = fma2(hb[q], hb[q], na * c);                             // :257
+                if constexpr (SCALAR) {                                           // objects.rs:217-222
+                    hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
+                    const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+                    disc[q] = hb[q] * hb[q] - (-na) * c;
+                } else {
+                    hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));               // :255
+                    const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;  // :256
+                    disc[q] = fma2(hb[q], hb[q], na * c);                         // :257
+                }
             }
             // acc = cand0 | cand1 | cand2 | cand3 as a strict chain: v_bitop3 computes
             // S0 | (~S1 & S2) (table 0xF2) in one op, so the group test is 4 VALU + 1 compare.
             uint32_t acc = cand(hb[0].x, disc[0].x);
-            if constexpr (!root2) {
+            if constexpr (!kDiscOnly) {
                 acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[0].y), sbits(hb[0].y), 0xF2);
                 acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[1].x), sbits(hb[1].x), 0xF2);
                 acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[1].y), sbits(hb[1].y), 0xF2);
@@ -265,9 +285,14 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
             for (uint32_t j = 0; j < 2; ++j) {
                 const T* v = &cur.v[4 * j];
                 const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
-                hb[j] = pk_dot(oc, d);                                     // :255
-                const T c = pk_len2(oc) - v[3];                            // :256
-                disc[j] = fma(hb[j], hb[j], -a * c);                       // :257
+                if constexpr (SCALAR) {                                    // objects.rs:217-222
+                    hb[j] = dot(oc, d);
+                    disc[j] = hb[j] * hb[j] - a * (len2(oc) - v[3]);
+                } else {
+                    hb[j] = pk_dot(oc, d);                                 // :255
+                    const T c = pk_len2(oc) - v[3];                        // :256
+                    disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
+                }
             }
             const uint32_t m0 = cand(hb[0], disc[0]), m1 = cand(hb[1], disc[1]);
             if (is_cand(m0 | m1)) {
@@ -284,9 +309,15 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     const V3<T> cen = mk(sg[0], sg[1], sg[2]);
     const V3<T> hp = mk(o.x + d.x * best_t, o.y + d.y * best_t, o.z + d.z * best_t);
     V3<T> nrm = sub(hp, cen);
-    const T len = sqrt(pk_len2(nrm));
-    nrm = mk(nrm.x / len, nrm.y / len, nrm.z / len);
-    const bool front = pk_dot(d, nrm) < T(0.0);
+    bool front;
+    if constexpr (SCALAR) {   // (location - center) / radius, HitRecord::new (objects.rs:242, 65-73)
+        nrm = dvs(nrm, sg[3]);
+        front = dot(d, nrm) < T(0.0);
+    } else {
+        const T len = sqrt(pk_len2(nrm));
+        nrm = mk(nrm.x / len, nrm.y / len, nrm.z / len);
+        front = pk_dot(d, nrm) < T(0.0);
+    }
     if (!front) nrm = neg(nrm);
     // Material::get_hit_result (materials.rs:54-147); scatter stream 2
     const MatT<T> m = q.mats[q.smat[best]];
@@ -323,193 +354,8 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     return true;
 }
 
-// Per-wave scratch in global memory (L2 / Infinity-Cache resident): SoA arrays of capacity P,
-// addressed as (wave-uniform base in SGPRs) + (field * P + position) * sizeof(T), so the loads
-// and stores use the SGPR-base + VGPR-offset form and no per-field pointer occupies registers.
-enum Field : uint32_t {
-    F_OX, F_OY, F_OZ, F_DX, F_DY, F_DZ, F_CR, F_CG, F_CB,   // active rays by position
-    F_TR, F_TG, F_TB,                                         // rays terminated this bounce, by terminated rank
-    F_VR, F_VG, F_VB,                                         // retired value by position
-    F_YV,                                                     // primary-ray y by position (quirk Q2)
-    F_NT                                                      // number of T fields; then 2 u32 fields:
-};
-// u32 fields after the T fields: sample id by position (RNG key), old position of terminated rays.
-constexpr uint32_t U_SID = 0, U_TPOS = 1;
-
-__host__ __device__ inline size_t scratch_bytes(uint32_t P, size_t tsz) {
-    return ((size_t)P * (F_NT * tsz + 8) + 255) & ~(size_t)255;
-}
-
-template <typename T> struct Scratch {
-    char* base;
-    uint32_t P;
-    __device__ __forceinline__ T& f(uint32_t field, uint32_t i) const {
-        return *(T*)(base + ((size_t)field * P + i) * sizeof(T));
-    }
-    __device__ __forceinline__ uint32_t& u(uint32_t field, uint32_t i) const {
-        return *(uint32_t*)(base + (size_t)F_NT * P * sizeof(T) + ((size_t)field * P + i) * 4u);
-    }
-};
-
 // Make this wave's earlier global stores visible to its later loads (other lanes, same wave).
 __device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// One wave renders one pixel at a time (persistent; pixels pulled from an atomic counter).
-// Per bounce k the n_k active rays sit at positions [0, n_k) of the wave's scratch; the wave
-// walks them in rounds of 64 (lane = position within the round), traces each against all
-// spheres, and compacts survivors in place with __ballot/popcount: a survivor's new position
-// (its rank) never exceeds its old one, and rounds run in order, so no position is overwritten
-// before it is read.  Terminated rays are appended to a dense list; once n_{k+1} is known,
-// their retire-rule values are written into the position-indexed value array.
-template <typename T, int W, bool ROOT2>
-__global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
-    // Only the sphere-loop operands come from the by-value `p` (hoisted to SGPRs); everything
-    // else is re-read through cold_args() where it is used, to keep SGPR pressure low.
-    __shared__ unsigned long long wcount[4][3];   // per-wave work counters
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform
-    if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
-
-    for (;;) {
-        const auto& q = *cold_args<T>();
-        uint32_t item = 0;
-        if (lane == 0) item = atomicAdd(q.counter, 1u);
-        item = __builtin_amdgcn_readfirstlane(item);
-        if (item >= q.n_items) break;
-        const uint32_t ri = item / q.col_count, ci = item % q.col_count;
-        const uint32_t row = q.row_begin + ri * q.row_step, col = q.col_begin + ci;
-        const uint32_t pix = row * q.W + col;
-        const uint32_t P = q.P, spp = q.spp, depth = q.depth, C = q.C;
-        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-        const Scratch<T> sc{q.scratch + (size_t)gw * q.scratch_stride, P};
-
-        // Retired-value init.  Positions [spp, P): missing lanes of a partial last chunk,
-        // disabled from the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424),
-        // zero primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel==0).
-        {
-            const V3<T> s0 = sky(T(0.0));
-            const bool white0 = q.s_sel == 0u;
-            for (uint32_t qi = lane; qi < P; qi += 64u) {
-                T vr = 0, vg = 0, vb = 0;
-                if (qi >= spp) {
-                    if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
-                    else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
-                }
-                sc.f(F_VR, qi) = vr; sc.f(F_VG, qi) = vg; sc.f(F_VB, qi) = vb;
-            }
-        }
-
-        uint32_t n = spp;     // active rays, at positions [0, n)
-        uint32_t Lcur = C;    // last_active_chunk (ray_tracing.rs:386)
-        for (uint32_t k = 0; k < depth; ++k) {
-            uint32_t nsurv = 0;
-            for (uint32_t base = 0; base < n; base += 64u) {
-                const uint32_t pos = base + lane;
-                const bool act = pos < n;
-                bool surv = false;
-                V3<T> o, d, c;
-                uint32_t sid = 0;
-                if (act) {
-                    if (k == 0) {
-                        camera_ray(p, col, row, pix, pos, o, d);
-                        c = mk(T(1.0), T(1.0), T(1.0));
-                        sid = pos;
-                        sc.f(F_YV, pos) = d.y;
-                    } else {
-                        o = mk(sc.f(F_OX, pos), sc.f(F_OY, pos), sc.f(F_OZ, pos));
-                        d = mk(sc.f(F_DX, pos), sc.f(F_DY, pos), sc.f(F_DZ, pos));
-                        c = mk(sc.f(F_CR, pos), sc.f(F_CG, pos), sc.f(F_CB, pos));
-                        sid = sc.u(U_SID, pos);
-                    }
-                    surv = bounce<T, ROOT2>(p, o, d, c, pix, sid, k);
-                }
-                const unsigned long long bal = __ballot(act && surv);
-                const uint32_t rank = nsurv + (uint32_t)__popcll(bal & lt_mask);
-                if (act) {
-                    if (surv) {   // stable compaction, ray_tracing.rs:430-458
-                        sc.f(F_OX, rank) = o.x; sc.f(F_OY, rank) = o.y; sc.f(F_OZ, rank) = o.z;
-                        sc.f(F_DX, rank) = d.x; sc.f(F_DY, rank) = d.y; sc.f(F_DZ, rank) = d.z;
-                        sc.f(F_CR, rank) = c.x; sc.f(F_CG, rank) = c.y; sc.f(F_CB, rank) = c.z;
-                        sc.u(U_SID, rank) = sid;
-                    } else {      // hit the sky (:421-424): keep colour + old position
-                        const uint32_t t = pos - rank;
-                        sc.f(F_TR, t) = c.x; sc.f(F_TG, t) = c.y; sc.f(F_TB, t) = c.z;
-                        sc.u(U_TPOS, t) = pos;
-                    }
-                }
-                nsurv += (uint32_t)__popcll(bal);
-            }
-            if (lane == 0) {
-                wcount[wave][0] += n;
-                wcount[wave][1] += 64u * ((n + 63u) / 64u);
-                wcount[wave][2] += 1u;
-            }
-            const auto& q2 = *cold_args<T>();
-            const uint32_t n_next = nsurv, nterm = n - nsurv;
-            const uint32_t Lnext = (k + 1 == q2.depth) ? 0u : (n_next + 3u) / 4u;
-            const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;   // positions retiring at bounce k
-            const bool U = q2.s_sel == (k & 1u);                // final read = this bounce's unsorted buffer
-            wave_mem_sync();
-            for (uint32_t t0 = 0; t0 < nterm; t0 += 64u) {
-                const uint32_t t = t0 + lane;
-                if (t < nterm) {
-                    const uint32_t pold = sc.u(U_TPOS, t), pnew = n_next + t;
-                    const V3<T> c = mk(sc.f(F_TR, t), sc.f(F_TG, t), sc.f(F_TB, t));
-                    if (U && pold >= lo && pold < hi) {
-                        const V3<T> s = sky(sc.f(F_YV, pold));
-                        sc.f(F_VR, pold) = c.x * s.x; sc.f(F_VG, pold) = c.y * s.y; sc.f(F_VB, pold) = c.z * s.z;
-                    }
-                    if (!U || pnew < lo || pnew >= hi) {
-                        const V3<T> s = sky(sc.f(F_YV, pnew));
-                        sc.f(F_VR, pnew) = c.x * s.x; sc.f(F_VG, pnew) = c.y * s.y; sc.f(F_VB, pnew) = c.z * s.z;
-                    }
-                }
-            }
-            wave_mem_sync();
-            n = n_next;
-            Lcur = Lnext;
-            if (n == 0) break;
-        }
-
-        // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
-        // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
-        T acc = T(0.0);
-        if (lane < 12u) {
-            const uint32_t ch = lane >> 2, l = lane & 3u;
-            // loads in batches of 16 (independent addresses in flight), adds strictly in order
-            uint32_t j = 0;
-            for (; j + 16 <= C; j += 16) {
-                T v[16];
-#pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = sc.f(F_VR + ch, 4 * (j + u) + l);
-#pragma unroll
-                for (int u = 0; u < 16; ++u) acc = acc + v[u];
-            }
-            for (; j < C; ++j) acc = acc + sc.f(F_VR + ch, 4 * j + l);
-        }
-        const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
-                s3 = __shfl(acc, (int)((lane + 3) & 63u));
-        if (lane < 12u && (lane & 3u) == 0u) {
-            const uint32_t ch = lane >> 2;
-            const T tot = (((T(0.0) + acc) + s1) + s2) + s3;
-            const T v = tot / (T)spp;                                   // renderer.rs:161
-            const auto& q3 = *cold_args<T>();
-            if (!(v <= T(2.0))) atomicOr(q3.err, 1u);                   // color.rs:55-57 assert
-            if (q3.rgb) q3.rgb[(size_t)item * 3 + ch] = q8(v);
-            if (q3.lin) q3.lin[(size_t)item * 3 + ch] = (double)v;
-        }
-    }
-    if (lane == 0) {
-        const auto& q = *cold_args<T>();
-        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-        unsigned long long* c = &q.segs[(gw & (kSegShards - 1)) * kSegStride];
-        atomicAdd(c + 0, wcount[wave][0]);
-        atomicAdd(c + 1, wcount[wave][1]);
-        atomicAdd(c + 2, wcount[wave][2]);
-    }
-}
-
 
 // ---------------------------------------------------------------------------------------------
 // Path regeneration.  Each ray of a pixel evolves independently of the others: bounce k of
@@ -526,8 +372,16 @@ __global__ __launch_bounds__(256, W) void trace_waves(KParams<T> p) {
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kSlots = 8;   // pixels a wave may have in flight (lane s holds slot s's metadata)
 
+// Semantics modes (RT_FLAG_MODE_*): which of the reference's renderers the kernel reproduces.
+enum Mode : int {
+    kModeV2 = 0,       // render_vectorized2 -> trace_vectorized2 (the live path; quirks Q2, Q3)
+    kModeV1 = 1,       // render_vectorized -> trace_vectorized (ray_tracing.rs:312-373): own value, final-ray sky
+    kModeScalar = 2,   // render -> trace_rays (ray_tracing.rs:264-306) + Color::average
+};
+
 // Per-wave scratch of trace_paths: the position-indexed value array (3 x P) for the pixel being
-// reduced, then kSlots record regions {y[P], c[3][P], e[P]} indexed by sample.
+// reduced, then kSlots record regions {y[P], c[3][P], e[P]} indexed by sample.  In the V1 and
+// scalar modes c holds each sample's final value (colour x sky of its own escaping ray, or 0).
 template <typename T> struct PScratch {
     char* base;        // wave-uniform
     uint32_t P, vbytes, sbytes;
@@ -555,7 +409,7 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
-template <typename T>
+template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item,
                                                           uint32_t* hist) {
     const auto& q = *cold_args<T>();
@@ -566,7 +420,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424) with a zero
     // primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel == 0).
     // Positions [0, spp) start at 0 (a ray still enabled at the end contributes black).
-    {
+    if (MODE == kModeV2) {
         const V3<T> s0 = sky(T(0.0));
         const bool white0 = q.s_sel == 0u;
         for (uint32_t qi = lane; qi < P; qi += 64u) {
@@ -587,7 +441,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     }
     wave_mem_sync();
     uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
-    for (uint32_t k = 0; k < K; ++k) {
+    for (uint32_t k = 0; k < (MODE == kModeV2 ? K : 0u); ++k) {
         if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
             kb = k;
             hist[lane] = 0;
@@ -634,24 +488,44 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     wave_mem_sync();
     // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
     // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
+    // V1: render_vectorized's packed_color + chunk (renderer.rs:120) is the same per-lane order,
+    // over each sample's own value (+0 for the disabled lanes of a partial chunk: black x sky).
+    // Scalar: Color::average (color.rs:66-85), one sequential sum over the samples.
+    auto val = [&](uint32_t ch, uint32_t pos) -> T {
+        if constexpr (MODE == kModeV2) return sc.v(ch, pos);
+        else return pos < spp ? sc.c(s, ch, pos) : T(0.0);
+    };
     T acc = T(0.0);
-    if (lane < 12u) {
+    if (MODE == kModeScalar) {
+        if (lane < 3u) {
+            uint32_t i = 0;
+            for (; i + 16 <= spp; i += 16) {
+                T v[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) v[u] = sc.c(s, lane, i + u);
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc = acc + v[u];
+            }
+            for (; i < spp; ++i) acc = acc + sc.c(s, lane, i);
+        }
+    } else if (lane < 12u) {
         const uint32_t ch = lane >> 2, l = lane & 3u;
         uint32_t j = 0;
         for (; j + 16 <= C; j += 16) {
             T v[16];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = sc.v(ch, 4 * (j + u) + l);
+            for (int u = 0; u < 16; ++u) v[u] = val(ch, 4 * (j + u) + l);
 #pragma unroll
             for (int u = 0; u < 16; ++u) acc = acc + v[u];
         }
-        for (; j < C; ++j) acc = acc + sc.v(ch, 4 * j + l);
+        for (; j < C; ++j) acc = acc + val(ch, 4 * j + l);
     }
     const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
             s3 = __shfl(acc, (int)((lane + 3) & 63u));
-    if (lane < 12u && (lane & 3u) == 0u) {
-        const uint32_t ch = lane >> 2;
-        const T tot = (((T(0.0) + acc) + s1) + s2) + s3;
+    const bool writer = MODE == kModeScalar ? lane < 3u : (lane < 12u && (lane & 3u) == 0u);
+    if (writer) {
+        const uint32_t ch = MODE == kModeScalar ? lane : lane >> 2;
+        const T tot = MODE == kModeScalar ? acc : (((T(0.0) + acc) + s1) + s2) + s3;
         const T v = tot / (T)spp;                                   // renderer.rs:161
         if (!(v <= T(2.0))) atomicOr(q.err, 1u);                    // color.rs:55-57 assert
         if (q.rgb) q.rgb[(size_t)item * 3 + ch] = q8(v);
@@ -664,7 +538,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
 // (cur, next sample cur_next), the busy-slot mask, and per-slot pixel/remaining-sample counts held
 // in lane s of two VGPRs.  Per iteration: hand free lanes new samples, trace one bounce for every
 // live ray (one sphere sweep for the whole wave), record terminations, finish completed pixels.
-template <typename T, int W, bool ROOT2>
+template <typename T, int W, bool ROOT2, int MODE = kModeV2>
 __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ unsigned long long wcount[4][3];
     __shared__ uint32_t s_hist[4][64];
@@ -727,13 +601,13 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             c = mk(T(1.0), T(1.0), T(1.0));
             k = 0;
             live = true;
-            sc.y(slot, sid) = d.y;
+            if (MODE == kModeV2) sc.y(slot, sid) = d.y;
         }
         if (__ballot(live) == 0ull) break;   // drained, and every slot finished
         // ---- one bounce for every live ray ----
         const bool act = live && k < depth;
         bool surv = false;
-        if (act) surv = bounce<T, ROOT2>(p, o, d, c, pix, sid, k);
+        if (act) surv = bounce<T, ROOT2, MODE == kModeScalar>(p, o, d, c, pix, sid, k);
         const unsigned long long bact = __ballot(act);
         if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
         // ---- terminations: record e (and the colour of a sky hit) ----
@@ -741,7 +615,13 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (term) {
             const bool skyhit = act && !surv;
             sc.e(slot, sid) = skyhit ? k : depth;
-            if (skyhit) { sc.c(slot, 0, sid) = c.x; sc.c(slot, 1, sid) = c.y; sc.c(slot, 2, sid) = c.z; }
+            if (MODE == kModeV2) {
+                if (skyhit) { sc.c(slot, 0, sid) = c.x; sc.c(slot, 1, sid) = c.y; sc.c(slot, 2, sid) = c.z; }
+            } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
+                V3<T> v = mk(T(0.0), T(0.0), T(0.0));
+                if (skyhit) { const V3<T> sk = sky(d.y); v = mk(c.x * sk.x, c.y * sk.y, c.z * sk.z); }
+                sc.c(slot, 0, sid) = v.x; sc.c(slot, 1, sid) = v.y; sc.c(slot, 2, sid) = v.z;
+            }
         }
         if (act && surv) k += 1u;
         live = live && !term;
@@ -754,7 +634,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (lane == s) slot_left -= (uint32_t)__popcll(m);
             if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
                 if (!synced) { wave_mem_sync(); synced = true; }
-                const uint32_t K = finish_pixel<T>(sc, s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
+                const uint32_t K = finish_pixel<T, MODE>(sc, s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
                 if (lane == 0) wcount[wave][2] += K;
                 busy &= ~(1u << s);
             }
@@ -903,11 +783,11 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
         cen[4 * i + 0] = (T)s->center[3 * i + 0];
         cen[4 * i + 1] = (T)s->center[3 * i + 1];
         cen[4 * i + 2] = (T)s->center[3 * i + 2];
-        cen[4 * i + 3] = r * r;   // self.radius.powi(2) in T (objects.rs:256)
+        cen[4 * i + 3] = r;       // signed radius (scalar-mode normal, objects.rs:242)
     }
     auto field = [&](uint32_t i, int f) -> T {   // dummies: centre 0, r^2 = -inf (never hit)
         if (i >= n) return f == 3 ? -std::numeric_limits<T>::infinity() : T(0);
-        return cen[4 * i + f];
+        return f == 3 ? cen[4 * i + 3] * cen[4 * i + 3] : cen[4 * i + f];   // r.powi(2) in T (objects.rs:256)
     };
     grp.assign((size_t)64 / sizeof(T) * (n_groups + 1), T(0));   // + 1 dummy group: prefetch target
     for (uint32_t i = 0; i < npad + G; ++i) {
@@ -1020,14 +900,13 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
     const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
-    static const bool use_waves = [] { const char* e = getenv("RT_KERNEL"); return e && !strcmp(e, "waves"); }();
-    void (*kern)(KParams<T>) = !use_waves ?
-        (r2 ? trace_paths<T, kWavesRoot2, true>
-           : (W >= 8 ? trace_paths<T, 8, false> : W >= 6 ? trace_paths<T, 6, false> : W >= 5 ? trace_paths<T, 5, false>
-            : W >= 4 ? trace_paths<T, 4, false> : trace_paths<T, 1, false>)) :
-        r2 ? trace_waves<T, kWavesRoot2, true>
-           : (W >= 8 ? trace_waves<T, 8, false> : W >= 6 ? trace_waves<T, 6, false> : W >= 5 ? trace_waves<T, 5, false>
-            : W >= 4 ? trace_waves<T, 4, false> : trace_waves<T, 1, false>);
+    void (*kern)(KParams<T>);
+    if (flags & RT_FLAG_MODE_SCALAR) kern = trace_paths<T, kWavesRoot2, false, kModeScalar>;
+    else if (flags & RT_FLAG_MODE_VECTORIZED)
+        kern = r2 ? trace_paths<T, kWavesRoot2, true, kModeV1> : trace_paths<T, kWavesRoot2, false, kModeV1>;
+    else if (r2) kern = trace_paths<T, kWavesRoot2, true>;
+    else kern = W >= 8 ? trace_paths<T, 8, false> : W >= 6 ? trace_paths<T, 6, false> : W >= 5 ? trace_paths<T, 5, false>
+              : W >= 4 ? trace_paths<T, 4, false> : trace_paths<T, 1, false>;
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));
     if (per_cu < 1) per_cu = 1;
@@ -1036,7 +915,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     if (nblocks > need) nblocks = need;
     p.vbytes = paths_vbytes(p.P, sizeof(T));
     p.sbytes = paths_sbytes(p.P, sizeof(T));
-    p.scratch_stride = use_waves ? scratch_bytes(p.P, sizeof(T)) : (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
+    p.scratch_stride = (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
     // Keep the scratch within a fixed budget: fewer resident waves for very large spp.
     const uint64_t kScratchBudget = 24ull << 30;
     const uint64_t max_blocks = kScratchBudget / (4 * p.scratch_stride);
@@ -1066,6 +945,9 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
                                uint32_t flags, const rt_tile_range* range, void* d_rgb8, void* d_linear, void* stream) {
     if (!c || !cam) return fail(RT_ERR_INVALID, "rt_render_async: NULL argument");
     if (spp == 0) return fail(RT_ERR_INVALID, "rt_render_async: spp == 0 (the reference panics: 0/0 in to_u8_array)");
+    if (flags & ~RT_FLAG_ALL) return fail(RT_ERR_INVALID, "rt_render_async: unknown flag bits");
+    if ((flags & RT_FLAG_MODE_VECTORIZED) && (flags & RT_FLAG_MODE_SCALAR))
+        return fail(RT_ERR_INVALID, "rt_render_async: RT_FLAG_MODE_VECTORIZED and RT_FLAG_MODE_SCALAR are exclusive");
     if (spp > (1u << 20)) return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp > 2^20");
     if (cam->image_width == 0 || cam->image_height == 0) return fail(RT_ERR_INVALID, "rt_render_async: empty image");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "image too large");

@@ -1,7 +1,11 @@
 // rt-render — the reference's binary (src/main.rs:27-74) on the MI355X sample loop.
 //
 //   rt-render [--scene scene.toml] [--width 3840] [--height 2160] [--spp 100] [--bounces 50]
-//             [--seed 0x5EED0001] [--f32] [--root2] [--out output.png|.ppm] [--dump-scene]
+//             [--seed 0x5EED0001] [--f32] [--root2] [--mode vectorized2|vectorized|scalar]
+//             [--out output.png|.ppm] [--dump-scene]
+//
+// --mode picks which of the reference's renderers is reproduced (include/rt_mi355x.h): the live
+// render_vectorized2 (default), render_vectorized, or the scalar render.
 //
 // Defaults are main.rs's hard-coded values (scene.toml in the working directory, 3840x2160, 50
 // bounces, 100 spp, camera from (16,2,18.5) looking at the origin, vfov 30, focal 10, no defocus,
@@ -79,11 +83,18 @@ int main(int argc, char** argv) {
         else if (a == "--seed") seed = std::stoull(next(), nullptr, 0);
         else if (a == "--f32") flags |= RT_FLAG_F32;
         else if (a == "--root2") flags |= RT_FLAG_ROOT2;
+        else if (a == "--mode") {
+            const std::string m = next();
+            flags &= ~(RT_FLAG_MODE_VECTORIZED | RT_FLAG_MODE_SCALAR);
+            if (m == "vectorized") flags |= RT_FLAG_MODE_VECTORIZED;
+            else if (m == "scalar") flags |= RT_FLAG_MODE_SCALAR;
+            else if (m != "vectorized2") { std::fprintf(stderr, "unknown mode %s\n", m.c_str()); return 2; }
+        }
         else if (a == "--out") out = next();
         else if (a == "--dump-scene") dump = true;
         else if (a == "-h" || a == "--help") {
             std::puts("rt-render [--scene scene.toml] [--width W] [--height H] [--spp S] [--bounces B] [--seed N] "
-                      "[--f32] [--root2] [--out output.png] [--dump-scene]");
+                      "[--f32] [--root2] [--mode vectorized2|vectorized|scalar] [--out output.png] [--dump-scene]");
             return 0;
         } else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }

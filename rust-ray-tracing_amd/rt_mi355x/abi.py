@@ -22,6 +22,9 @@ RT_DIELECTRIC = 2
 
 RT_FLAG_F32 = 0x1
 RT_FLAG_ROOT2 = 0x2
+RT_FLAG_MODE_VECTORIZED = 0x4   # render_vectorized -> trace_vectorized semantics
+RT_FLAG_MODE_SCALAR = 0x8       # render -> trace_rays semantics
+RT_FLAG_ALL = 0xF
 
 
 class RtMaterial(ctypes.Structure):

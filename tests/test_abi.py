@@ -119,3 +119,13 @@ def test_no_gpu_fails_loudly():
     assert lib.rt_last_error()
     with pytest.raises(rt.RtError):
         rt.GpuRenderer(lib=lib)
+
+
+def test_header_constants_match_python_mirror():
+    """Every RT_* #define in include/rt_mi355x.h has the same value in rt_mi355x.abi."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "rt_mi355x.h")).read()
+    defs = dict(re.findall(r"#define\s+(RT_[A-Z0-9_]+)\s+(0x[0-9A-Fa-f]+|\d+)u?\b", hdr))
+    assert {"RT_FLAG_F32", "RT_FLAG_ROOT2", "RT_FLAG_MODE_VECTORIZED", "RT_FLAG_MODE_SCALAR", "RT_FLAG_ALL"} <= set(defs)
+    for name, val in defs.items():
+        assert getattr(abi, name) == int(val, 0), name
