@@ -47,14 +47,23 @@ class GpuRenderer(Renderer):
     """Drop-in for TileRenderer: renders the whole image on one MI355X via rt_render_async.
 
     seed: 64-bit key of the counter-based RNG (the reference's thread_rng is unseedable);
-    precision: "f64" (reference arithmetic) or "f32"; root2: quirk Q1 off.
+    precision: "f64" (reference arithmetic) or "f32"; root2: quirk Q1 off;
+    mode: which reference renderer to reproduce — "vectorized2" (the live render_vectorized2,
+    default), "vectorized" (render_vectorized) or "scalar" (render); see include/rt_mi355x.h.
     """
 
-    def __init__(self, device=0, seed=0x5EED0001, precision="f64", root2=False, lib=None):
+    MODES = {"vectorized2": 0, "vectorized": abi.RT_FLAG_MODE_VECTORIZED, "scalar": abi.RT_FLAG_MODE_SCALAR}
+
+    def __init__(self, device=0, seed=0x5EED0001, precision="f64", root2=False, mode="vectorized2", lib=None):
+        if mode not in self.MODES:
+            raise ValueError(f"unknown mode {mode!r} (one of {sorted(self.MODES)})")
+        if precision not in ("f64", "f32"):
+            raise ValueError(f"unknown precision {precision!r}")
         self.lib = lib or abi.load_library()
         self.device = device
         self.seed = seed
-        self.flags = (abi.RT_FLAG_F32 if precision == "f32" else 0) | (abi.RT_FLAG_ROOT2 if root2 else 0)
+        self.flags = ((abi.RT_FLAG_F32 if precision == "f32" else 0) | (abi.RT_FLAG_ROOT2 if root2 else 0)
+                      | self.MODES[mode])
         self.ctx = ctypes.c_void_p()
         abi.check(self.lib, self.lib.rt_context_create(device, ctypes.byref(self.ctx)))
         self._scene_key = None
