@@ -95,7 +95,7 @@ template <typename T> struct KParams {
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
-constexpr int kWavesF64 = 5;
+constexpr int kWavesF64 = 4;
 constexpr int kWavesRoot2 = 6;  // the Q1-off (scalar semantics) variant
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
@@ -124,33 +124,6 @@ template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args() {
     return k;
 }
 
-// Camera::get_ray, ray_tracing.rs:77-89 (jitter stream 0, disk stream 1).
-template <typename T>
-__device__ __forceinline__ void camera_ray(const KParams<T>& p0, uint32_t col, uint32_t row, uint32_t pix,
-                                           uint32_t s, V3<T>& o, V3<T>& d) {
-    cptr<KParams<T>> pk = cold_args<T>();
-    const auto& p = *pk;
-    const U4 r = philox(s, pix, 0u, 0u, p.k0, p.k1);
-    const T xo = u01a(r, T(0)), yo = u01b(r, T(0));
-    const T s1 = ((T)col + xo) / (T)p.W;
-    const T s2 = ((T)row + yo) / (T)p.H;
-    const V3<T> vu = mk(p.vu[0], p.vu[1], p.vu[2]), vv = mk(p.vv[0], p.vv[1], p.vv[2]);
-    const V3<T> pc = add(mk(p.ulc[0], p.ulc[1], p.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
-    T dx = 0, dy = 0;  // random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2
-    // With zero defocus vectors and no -0.0 in the camera centre, du*dx + dv*dy + center == center
-    // for every finite disk sample, so the draw cannot change a bit of the result: skip it.
-    for (uint32_t i = 0; i < (p.flags & kFlagPinholeInternal ? 0u : 256u); ++i) {
-        const U4 q = philox(s, pix, i, 1u, p.k0, p.k1);
-        const T x = T(2.0) * u01a(q, T(0)) - T(1.0);
-        const T y = T(2.0) * u01b(q, T(0)) - T(1.0);
-        if (x * x + y * y <= T(1.0)) { dx = x; dy = y; break; }
-    }
-    const V3<T> orig = add(add(mul(mk(p.du[0], p.du[1], p.du[2]), dx), mul(mk(p.dv[0], p.dv[1], p.dv[2]), dy)),
-                           mk(p.center[0], p.center[1], p.center[2]));
-    o = orig;
-    d = unit(sub(pc, orig));
-}
-
 // Walk the sphere groups with a two-deep scalar-load pipeline over two SGPR buffers (no
 // per-group SGPR copies).  Scalar loads return out of order, so any use waits lgkmcnt(0): the
 // next group's load is pinned (sched_barrier) BEFORE the current group's math and waited right
@@ -159,6 +132,10 @@ __device__ __forceinline__ void camera_ray(const KParams<T>& p0, uint32_t col, u
 template <typename T, typename F>
 __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
     SphGroup<T> A = load_group(f, 0);
+    // Wait for the first group here: otherwise the loop header inherits its pending load and the
+    // compiler's wait before the first use also waits for the group just prefetched in the body.
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
     uint32_t g = 0;
     for (; g + 1 < ng; g += 2) {
         const SphGroup<T> B = load_group(f, g + 1);
@@ -175,14 +152,13 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
     if (g < ng) group(A, g);
 }
 
-// One bounce of one enabled ray: the object loop of trace_vectorized2 (ray_tracing.rs:399-403)
-// + the per-lane material step (:406-426).  Returns true if the ray hit (and was scattered).
-// SCALAR selects Sphere::hit + Scene::hit + HitRecord::new (objects.rs:216-247, ray_tracing.rs:231-235,
-// objects.rs:65-83): no FMA, both roots, root = (-hb -/+ sd) / a, the first minimum wins ties, and
-// the normal is (p - c) / radius with the signed radius.  Otherwise hit_packed + PackedHitRecords.
+// The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
+// index of the nearest valid hit (-1: the sky, :421-424) and its t.
+// SCALAR selects Sphere::hit + Scene::hit (objects.rs:216-247, ray_tracing.rs:231-235): no FMA,
+// both roots, root = (-hb -/+ sd) / a, the first minimum wins ties.  Otherwise hit_packed +
+// PackedHitRecords::update (objects.rs:249-290, 140-155).
 template <typename T, bool root2, bool SCALAR = false>
-__device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, V3<T>& col, uint32_t pix,
-                                       uint32_t sid, uint32_t k) {
+__device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, const V3<T>& d, T& t_out) {
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254 (loop-invariant)
     T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
@@ -215,8 +191,11 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
     // Spheres stream through the scalar cache in 64-byte groups; group g+1 is requested before
     // group g is tested so the K$ latency hides behind the group's VALU work.
     // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
-    cptr<T> f = (cptr<T>)__builtin_assume_aligned(p.sph, 64);
-    const uint32_t ng = p.n_groups;
+    // Read through the laundered kernarg pointer at each sweep, so the sphere pointer and count do
+    // not hold SGPRs across the persistent loop (they were spilled to VGPR lanes, 2 VALU a group).
+    const auto& qa = *cold_args<T>();
+    cptr<T> f = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
+    const uint32_t ng = qa.n_groups;
     // Candidate filter, branch-free, on sign bits: cand(hb, disc) = ~bits(disc) & bits(hb) has its
     // sign bit set iff disc >= +0 and hb <= -0 — the only case in which root1 = (-hb - sqrt(disc))
     // * inv_a can be valid (root1 > 0 needs -hb > 0; NaNs never give a valid root).  disc is never
@@ -294,45 +273,86 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
                     disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
                 }
             }
-            const uint32_t m0 = cand(hb[0], disc[0]), m1 = cand(hb[1], disc[1]);
-            if (is_cand(m0 | m1)) {
+            uint32_t acc = cand(hb[0], disc[0]);
+            if constexpr (!kDiscOnly) acc = __builtin_amdgcn_bitop3_b32(acc, sbits(disc[1]), sbits(hb[1]), 0xF2);
+            else acc = acc | cand(hb[1], disc[1]);
+            if (is_cand(acc)) {
                 if (cand_f(hb[0], disc[0])) hit(hb[0], disc[0], 2 * g);
                 if (cand_f(hb[1], disc[1])) hit(hb[1], disc[1], 2 * g + 1);
             }
         };
         sphere_loop(f, ng, group);
     }
-    if (best < 0) return false;      // sky: ray_tracing.rs:421-424
+    t_out = best_t;
+    return best;
+}
+
+// The per-lane "next ray" stage.  Fresh lanes run Camera::get_ray (ray_tracing.rs:77-89; jitter
+// stream 0, disk stream 1); lanes that hit at bounce k run PackedHitRecords::finalize
+// (objects.rs:157-162) and Material::get_hit_result (materials.rs:54-147; stream 2).  Both draw one
+// Philox block and normalise one vector (v / sqrt(|v|^2): unit() for the camera direction, the
+// finalize normal), so the wave issues those once per iteration, not once per role.
+// SCALAR: HitRecord::new's normal is (p - c) / radius (objects.rs:242, 65-73).
+template <typename T, bool SCALAR>
+__device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy, uint32_t pix, uint32_t sid,
+                                         uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
     const auto& q = *cold_args<T>();
-    // PackedHitRecords::finalize (objects.rs:157-162); normal = at_t(t) - center (:279-280)
-    const T* sg = q.cen + 4 * best;
-    const V3<T> cen = mk(sg[0], sg[1], sg[2]);
-    const V3<T> hp = mk(o.x + d.x * best_t, o.y + d.y * best_t, o.z + d.z * best_t);
-    V3<T> nrm = sub(hp, cen);
-    bool front;
-    if constexpr (SCALAR) {   // (location - center) / radius, HitRecord::new (objects.rs:242, 65-73)
-        nrm = dvs(nrm, sg[3]);
-        front = dot(d, nrm) < T(0.0);
+    const U4 r = philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q.k0, q.k1);
+    const T ua = u01a(r, T(0)), ub = u01b(r, T(0));
+    V3<T> vec, base;
+    T l2, rad = T(1.0);
+    if (cam) {
+        const T s1 = ((T)colx + ua) / (T)q.W;
+        const T s2 = ((T)rowy + ub) / (T)q.H;
+        const V3<T> vu = mk(q.vu[0], q.vu[1], q.vu[2]), vv = mk(q.vv[0], q.vv[1], q.vv[2]);
+        const V3<T> pc = add(mk(q.ulc[0], q.ulc[1], q.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
+        const V3<T> center = mk(q.center[0], q.center[1], q.center[2]);
+        if (q.flags & kFlagPinholeInternal) {
+            // Zero defocus vectors and no -0.0 in the centre (checked on the host): du*dx + dv*dy
+            // + center == center for every disk sample, so the draw cannot change a bit.
+            base = center;
+        } else {
+            T dx = 0, dy = 0;   // random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2
+            for (uint32_t i = 0; i < 256u; ++i) {
+                const U4 qq = philox(sid, pix, i, 1u, q.k0, q.k1);
+                const T x = T(2.0) * u01a(qq, T(0)) - T(1.0);
+                const T y = T(2.0) * u01b(qq, T(0)) - T(1.0);
+                if (x * x + y * y <= T(1.0)) { dx = x; dy = y; break; }
+            }
+            base = add(add(mul(mk(q.du[0], q.du[1], q.du[2]), dx), mul(mk(q.dv[0], q.dv[1], q.dv[2]), dy)), center);
+        }
+        vec = sub(pc, base);
+        l2 = len2(vec);                                   // unit(): Vec3::length (geometry.rs:106-112)
     } else {
-        const T len = sqrt(pk_len2(nrm));
-        nrm = mk(nrm.x / len, nrm.y / len, nrm.z / len);
-        front = pk_dot(d, nrm) < T(0.0);
+        const T* sg = q.cen + 4 * hit_i;
+        base = mk(o.x + d.x * hit_t, o.y + d.y * hit_t, o.z + d.z * hit_t);   // at_t
+        vec = sub(base, mk(sg[0], sg[1], sg[2]));        // normal = at_t(t) - center (objects.rs:279-280)
+        l2 = pk_len2(vec);
+        if constexpr (SCALAR) rad = sg[3];
     }
+    const T len = (SCALAR && !cam) ? rad : sqrt(l2);
+    const V3<T> u = mk(vec.x / len, vec.y / len, vec.z / len);
+    if (cam) {
+        o = base;
+        d = u;
+        c = mk(T(1.0), T(1.0), T(1.0));
+        return;
+    }
+    V3<T> nrm = u;
+    const bool front = (SCALAR ? dot(d, nrm) : pk_dot(d, nrm)) < T(0.0);
     if (!front) nrm = neg(nrm);
-    // Material::get_hit_result (materials.rs:54-147); scatter stream 2
-    const MatT<T> m = q.mats[q.smat[best]];
-    const U4 r = philox(sid, pix, k, 2u, q.k0, q.k1);
+    const MatT<T> m = q.mats[q.smat[hit_i]];
     V3<T> nd;
     if (m.kind != RT_DIELECTRIC) {
         // One random_unit_vector for both kinds (a wave usually holds both: one evaluation, not two).
-        const V3<T> rv = unit_vec(u01a(r, T(0)), u01b(r, T(0)));
+        const V3<T> rv = unit_vec(ua, ub);
         if (m.kind == RT_LAMBERTIAN) {
             nd = add(rv, nrm);
             if (near_zero(nd)) nd = nrm;
         } else {
             nd = add(reflect(d, nrm), mul(rv, m.fuzz));
         }
-        col = mk(col.x * m.ar, col.y * m.ag, col.z * m.ab);
+        c = mk(c.x * m.ar, c.y * m.ag, c.z * m.ab);
     } else {
         const T ratio = front ? m.inv_ior : m.ior;
         const V3<T> nn = m.hollow ? neg(nrm) : nrm;
@@ -344,14 +364,13 @@ __device__ __forceinline__ bool bounce(const KParams<T>& p, V3<T>& o, V3<T>& d, 
             const T m1 = T(1.0) - ct;
             const T m2 = m1 * m1;
             const T m5 = m1 * (m2 * m2);
-            refl = r0 + (T(1.0) - r0) * m5 > u01a(r, T(0));
+            refl = r0 + (T(1.0) - r0) * m5 > ua;
         }
         nd = refl ? reflect(d, nn) : refract(d, nn, ratio);
-        col = mk(col.x * T(1.0), col.y * T(1.0), col.z * T(1.0));
+        c = mk(c.x * T(1.0), c.y * T(1.0), c.z * T(1.0));
     }
-    o = hp;
+    o = base;
     d = nd;
-    return true;
 }
 
 // Make this wave's earlier global stores visible to its later loads (other lanes, same wave).
@@ -398,6 +417,17 @@ template <typename T> struct PScratch {
         return *(uint32_t*)(base + vbytes + s * sbytes + 4u * P * (uint32_t)sizeof(T) + i * 4u);
     }
 };
+// This wave's scratch view, re-derived from the kernel arguments where it is used (it is needed
+// only at record writes and pixel completion, so it does not hold SGPRs across the sphere sweep).
+template <typename T> __device__ __forceinline__ PScratch<T> wave_scratch(uint32_t wave) {
+    const auto& q = *cold_args<T>();
+    const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
+    return PScratch<T>{q.scratch + (size_t)gw * q.scratch_stride, q.P, q.vbytes, q.sbytes};
+}
+
+// Wave-uniform issue state, parked in LDS between refills for the same reason.
+struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, drained, pad; };
+
 __host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t tsz) { return (3u * P * tsz + 255u) & ~255u; }
 __host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz) { return (P * (4u * tsz + 4u) + 255u) & ~255u; }
 
@@ -549,25 +579,28 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     if (lane < 4) g_kst[wave][lane] = 0;
 #endif
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    PScratch<T> sc;
-    uint32_t spp, depth, n_items;
-    {
-        const auto& q = *cold_args<T>();
-        const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-        sc = PScratch<T>{q.scratch + (size_t)gw * q.scratch_stride, q.P, q.vbytes, q.sbytes};
-        spp = q.spp; depth = q.depth; n_items = q.n_items;
-    }
+    __shared__ IssueState s_is[4];
+    if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u};
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
     uint32_t sid = 0, k = 0, slot = 0, pix = 0;
     bool live = false;
+    bool scat = false;                 // hit at bounce k last iteration, still below depth: scatter now
+    int hit_i = -1;
+    T hit_t = T(0);
     uint32_t slot_item = 0, slot_left = 0;   // lane s < kSlots: pixel item and unfinished samples of slot s
-    uint32_t busy = 0, cur = 0, cur_next = spp, cur_pix = 0, cur_row = 0, cur_col = 0;
-    bool drained = false;
     for (;;) {
         // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
+        const uint32_t spp = cold_args<T>()->spp, depth = cold_args<T>()->depth;
         bool fresh = false;
         uint32_t frow = 0, fcol = 0;
         unsigned long long freem = __ballot(!live);
+        uint32_t busy = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
+        uint32_t cur = __builtin_amdgcn_readfirstlane(s_is[wave].cur);
+        uint32_t cur_next = __builtin_amdgcn_readfirstlane(s_is[wave].cur_next);
+        uint32_t cur_pix = __builtin_amdgcn_readfirstlane(s_is[wave].cur_pix);
+        uint32_t cur_row = __builtin_amdgcn_readfirstlane(s_is[wave].cur_row);
+        uint32_t cur_col = __builtin_amdgcn_readfirstlane(s_is[wave].cur_col);
+        bool drained = __builtin_amdgcn_readfirstlane(s_is[wave].drained) != 0u;
         while (freem != 0ull && !drained) {
             if (cur_next == spp) {
                 const uint32_t avail = ~busy & ((1u << kSlots) - 1u);
@@ -576,7 +609,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 uint32_t item = 0;
                 if (lane == 0) item = atomicAdd(q.counter, 1u);
                 item = __builtin_amdgcn_readfirstlane(item);
-                if (item >= n_items) { drained = true; break; }
+                if (item >= q.n_items) { drained = true; break; }
                 const uint32_t s = __builtin_ctz(avail);
                 const uint32_t ri = item / q.col_count, ci = item % q.col_count;
                 cur_row = q.row_begin + ri * q.row_step;
@@ -595,25 +628,32 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             freem &= ~__ballot(mine);
             cur_next += take;
         }
+        if (lane == 0) s_is[wave] = IssueState{busy, cur, cur_next, cur_pix, cur_row, cur_col, drained ? 1u : 0u, 0u};
         KSTAT(3, __ballot(fresh) != 0ull ? 1u : 0u);
-        if (fresh) {   // Camera::get_ray (ray_tracing.rs:77-89); primary y kept for quirk Q2
-            camera_ray(p, fcol, frow, pix, sid, o, d);
-            c = mk(T(1.0), T(1.0), T(1.0));
+        // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
+        if (fresh || scat) next_ray<T, MODE == kModeScalar>(fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
+        if (fresh) {
             k = 0;
             live = true;
-            if (MODE == kModeV2) sc.y(slot, sid) = d.y;
+            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
+        } else if (scat) {
+            k += 1u;
         }
         if (__ballot(live) == 0ull) break;   // drained, and every slot finished
-        // ---- one bounce for every live ray ----
+        // ---- one sphere sweep for every live ray ----
         const bool act = live && k < depth;
-        bool surv = false;
-        if (act) surv = bounce<T, ROOT2, MODE == kModeScalar>(p, o, d, c, pix, sid, k);
+        hit_i = -1;
+        if (act) hit_i = nearest_hit<T, ROOT2, MODE == kModeScalar>(p, o, d, hit_t);
         const unsigned long long bact = __ballot(act);
         if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
         // ---- terminations: record e (and the colour of a sky hit) ----
-        const bool term = live && (!act || !surv || k + 1 == depth);
+        const bool skyhit = act && hit_i < 0;
+        // A hit at the last bounce is not scattered: the ray stays enabled and reads black
+        // whatever its colour (ray_tracing.rs:495-497), and the scatter draws nothing observable.
+        const bool term = live && (!act || skyhit || k + 1 == depth);
+        scat = act && hit_i >= 0 && k + 1 < depth;
         if (term) {
-            const bool skyhit = act && !surv;
+            const PScratch<T> sc = wave_scratch<T>(wave);
             sc.e(slot, sid) = skyhit ? k : depth;
             if (MODE == kModeV2) {
                 if (skyhit) { sc.c(slot, 0, sid) = c.x; sc.c(slot, 1, sid) = c.y; sc.c(slot, 2, sid) = c.z; }
@@ -623,7 +663,6 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 sc.c(slot, 0, sid) = v.x; sc.c(slot, 1, sid) = v.y; sc.c(slot, 2, sid) = v.z;
             }
         }
-        if (act && surv) k += 1u;
         live = live && !term;
         unsigned long long tm = __ballot(term);
         bool synced = false;
@@ -634,9 +673,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (lane == s) slot_left -= (uint32_t)__popcll(m);
             if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
                 if (!synced) { wave_mem_sync(); synced = true; }
-                const uint32_t K = finish_pixel<T, MODE>(sc, s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
+                const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
+                                                         s_hist[wave]);
                 if (lane == 0) wcount[wave][2] += K;
-                busy &= ~(1u << s);
+                const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
+                if (lane == 0) s_is[wave].busy = b & ~(1u << s);
             }
         }
     }
