@@ -123,6 +123,13 @@ template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args() {
     asm volatile("" : "+s"(k));
     return k;
 }
+// Same, but ordered after `dep` is computed: loads through it cannot be hoisted above that value's
+// producer (used to keep the camera constants out of SGPRs while a Philox block is in flight).
+template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args_after(uint32_t dep) {
+    cptr<KParams<T>> k = (cptr<KParams<T>>)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k) : "v"(dep));
+    return k;
+}
 
 // Walk the sphere groups with a two-deep scalar-load pipeline over two SGPR buffers (no
 // per-group SGPR copies).  Scalar loads return out of order, so any use waits lgkmcnt(0): the
@@ -296,8 +303,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 template <typename T, bool SCALAR>
 __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy, uint32_t pix, uint32_t sid,
                                          uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
-    const auto& q = *cold_args<T>();
-    const U4 r = philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q.k0, q.k1);
+    const U4 r = [&] {
+        const auto& q0 = *cold_args<T>();
+        return philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
+    }();
+    const auto& q = *cold_args_after<T>(r.a ^ r.b);
     const T ua = u01a(r, T(0)), ub = u01b(r, T(0));
     V3<T> vec, base;
     T l2, rad = T(1.0);
