@@ -324,7 +324,12 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         } else {
             T dx = 0, dy = 0;   // random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2
             for (uint32_t i = 0; i < 256u; ++i) {
-                const U4 qq = philox(sid, pix, i, 1u, q.k0, q.k1);
+                // Only cameras with defocus get here.  Re-launder the key each draw: hoisted, its
+                // 20-word round-key schedule held SGPRs across the whole camera stage and spilled
+                // the camera constants on every iteration, pinhole or not.
+                uint32_t k0 = q.k0, k1 = q.k1;
+                asm volatile("" : "+s"(k0), "+s"(k1));
+                const U4 qq = philox(sid, pix, i, 1u, k0, k1);
                 const T x = T(2.0) * u01a(qq, T(0)) - T(1.0);
                 const T y = T(2.0) * u01b(qq, T(0)) - T(1.0);
                 if (x * x + y * y <= T(1.0)) { dx = x; dy = y; break; }
