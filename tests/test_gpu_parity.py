@@ -6,6 +6,7 @@ linear colours must be BIT-IDENTICAL in both fp64 and fp32 mode, and RGB8 byte-i
 Tolerance stated for the record: 0 ulp (we assert array_equal).
 """
 import ctypes
+import math
 
 import numpy as np
 import pytest
@@ -329,3 +330,27 @@ def test_full_size_8gpu_configs(renderer, config, stride, flags):
                                    precision="f32" if flags & abi.RT_FLAG_F32 else "f64")
     np.testing.assert_array_equal(lin[idx], lin_o)
     assert 0.2 < lin.mean() < 0.9
+
+
+# ---- cameras off the pinhole shortcut (Camera::get_ray's disk draw, ray_tracing.rs:80-86) ----
+def _cam(w, h, **kw):
+    args = dict(rt.MAIN_CAMERA)
+    args.update(kw)
+    return rt.camera_new_py(w, h, **args)
+
+
+@pytest.mark.parametrize("mode", [0] + MODES)
+@pytest.mark.parametrize("prec", [0, abi.RT_FLAG_F32])
+def test_defocus_camera(renderer, scene_100, mode, prec):
+    """defocus_angle > 0: every primary ray has its own origin on the lens disk (rejection
+    sampling on stream 1), so the kernel takes the general camera path."""
+    assert_parity(renderer, scene_100, _cam(24, 14, defocus_angle=2.0), 50, 12, mode | prec)
+
+
+@pytest.mark.parametrize("prec", [0, abi.RT_FLAG_F32])
+def test_negative_zero_camera_centre(renderer, scene_100, prec):
+    """No defocus but a -0.0 in the camera centre: du*dx + dv*dy + center turns -0.0 into +0.0,
+    so the host must not take the pinhole shortcut (origin == center) — results stay exact."""
+    cam = _cam(24, 14, center=(-0.0, 2.0, 18.5), look_at=(0.0, 0.0, 0.0))
+    assert cam.center[0] == 0.0 and math.copysign(1.0, cam.center[0]) < 0
+    assert_parity(renderer, scene_100, cam, 50, 12, prec)
