@@ -90,13 +90,14 @@ template <typename T> struct KParams {
     char* scratch;             // per-wave scratch regions
     size_t scratch_stride;
     uint32_t vbytes, sbytes;   // trace_paths: value-array bytes, per-slot record bytes (PScratch)
+    const T* camsph;           // camera-origin table {oc, c} in the sph layout (pinhole launches)
 };
 
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
 constexpr int kWavesF64 = 4;
-constexpr int kWavesRoot2 = 6;  // the Q1-off (scalar semantics) variant
+template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
 // Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..6.
@@ -164,7 +165,9 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
 // SCALAR selects Sphere::hit + Scene::hit (objects.rs:216-247, ray_tracing.rs:231-235): no FMA,
 // both roots, root = (-hb -/+ sd) / a, the first minimum wins ties.  Otherwise hit_packed +
 // PackedHitRecords::update (objects.rs:249-290, 140-155).
-template <typename T, bool root2, bool SCALAR = false>
+// CAMT: the ray starts at the camera centre and the sweep reads the camera-origin table
+// (build_cam_table): oc and c come precomputed, bit-identical to the per-ray values.
+template <typename T, bool root2, bool SCALAR = false, bool CAMT = false>
 __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, const V3<T>& d, T& t_out) {
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254 (loop-invariant)
@@ -201,7 +204,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     // Read through the laundered kernarg pointer at each sweep, so the sphere pointer and count do
     // not hold SGPRs across the persistent loop (they were spilled to VGPR lanes, 2 VALU a group).
     const auto& qa = *cold_args<T>();
-    cptr<T> f = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
+    cptr<T> f = (cptr<T>)__builtin_assume_aligned(CAMT ? qa.camsph : qa.sph, 64);
     const uint32_t ng = qa.n_groups;
     // Candidate filter, branch-free, on sign bits: cand(hb, disc) = ~bits(disc) & bits(hb) has its
     // sign bit set iff disc >= +0 and hb <= -0 — the only case in which root1 = (-hb - sqrt(disc))
@@ -230,6 +233,17 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 #pragma unroll
             for (uint32_t q = 0; q < 2; ++q) {
                 const T* v = &cur.v[8 * q];
+                if constexpr (CAMT) {   // {ocx, ocy, ocz, c} pairs from the camera-origin table
+                    const f2 ocx = {v[0], v[1]}, ocy = {v[2], v[3]}, ocz = {v[4], v[5]}, c = {v[6], v[7]};
+                    if constexpr (SCALAR) {
+                        hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
+                        disc[q] = hb[q] * hb[q] - (-na) * c;
+                    } else {
+                        hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));
+                        disc[q] = fma2(hb[q], hb[q], na * c);
+                    }
+                    continue;
+                }
                 const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
                 const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
                 if constexpr (SCALAR) {                                           // objects.rs:217-222
@@ -270,6 +284,12 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 #pragma unroll
             for (uint32_t j = 0; j < 2; ++j) {
                 const T* v = &cur.v[4 * j];
+                if constexpr (CAMT) {   // {ocx, ocy, ocz, c} from the camera-origin table
+                    const V3<T> oc = mk(v[0], v[1], v[2]);
+                    hb[j] = SCALAR ? dot(oc, d) : pk_dot(oc, d);
+                    disc[j] = SCALAR ? hb[j] * hb[j] - a * v[3] : fma(hb[j], hb[j], -a * v[3]);
+                    continue;
+                }
                 const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
                 if constexpr (SCALAR) {                                    // objects.rs:217-222
                     hb[j] = dot(oc, d);
@@ -388,6 +408,29 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
     d = nd;
 }
 
+// Camera-origin sphere table for pinhole launches.  Every primary ray starts at the camera centre
+// (the host checked that the origin is the centre bit for bit), so oc = o - c and c = |oc|^2 - r^2
+// (objects.rs:252, 256; scalar: 217, 221) are the same for all of them.  Computed once per launch
+// with the same operations, in the sph group layout with {cx, cy, cz, r^2} -> {ocx, ocy, ocz, c};
+// a dummy (r^2 = -inf) gets c = +inf, so its discriminant is still -inf.
+template <typename T, bool SCALAR>
+__global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, T ox, T oy, T oz) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    constexpr uint32_t G = kGroup<T>, NE = 64 / sizeof(T);
+    const uint32_t g = i / G, j = i % G;
+    auto at = [&](uint32_t f) -> uint32_t {
+        return sizeof(T) == 4 ? g * NE + 8 * (j / 2) + 2 * f + (j % 2) : g * NE + 4 * j + f;
+    };
+    const T cx = sph[at(0)], cy = sph[at(1)], cz = sph[at(2)], r2 = sph[at(3)];
+    const T ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
+    const T c = SCALAR ? ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2 : fma(ocz, ocz, fma(ocy, ocy, ocx * ocx)) - r2;
+    cam[at(0)] = ocx;
+    cam[at(1)] = ocy;
+    cam[at(2)] = ocz;
+    cam[at(3)] = c;
+}
+
 // Make this wave's earlier global stores visible to its later loads (other lanes, same wave).
 __device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -441,7 +484,7 @@ template <typename T> __device__ __forceinline__ PScratch<T> wave_scratch(uint32
 }
 
 // Wave-uniform issue state, parked in LDS between refills for the same reason.
-struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, drained, pad; };
+struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, drained, qhead, qcount; };
 
 __host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t tsz) { return (3u * P * tsz + 255u) & ~255u; }
 __host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz) { return (P * (4u * tsz + 4u) + 255u) & ~255u; }
@@ -583,10 +626,23 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
 // (cur, next sample cur_next), the busy-slot mask, and per-slot pixel/remaining-sample counts held
 // in lane s of two VGPRs.  Per iteration: hand free lanes new samples, trace one bounce for every
 // live ray (one sphere sweep for the whole wave), record terminations, finish completed pixels.
-template <typename T, int W, bool ROOT2, int MODE = kModeV2>
+//
+// CAMQ (pinhole cameras, depth >= 1): primary rays are not mixed into the per-lane sweep.  They are
+// traced in full-wave camera batches against the camera-origin table (5 instead of 12 packed ops
+// per sphere pair); misses terminate on the spot, hits wait in a per-wave LDS queue and free lanes
+// pop them as rays whose bounce-0 scatter is pending.  Every ray still meets every sphere.
+constexpr uint32_t kQCap = 128;   // camera-batch queue entries per wave (a batch adds at most 64)
+
+template <typename T, int W, bool ROOT2, int MODE = kModeV2, bool CAMQ = false>
 __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
+    constexpr bool SC = MODE == kModeScalar;
+    constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? kQCap : 1;
     __shared__ unsigned long long wcount[4][3];
     __shared__ uint32_t s_hist[4][64];
+    __shared__ IssueState s_is[4];
+    __shared__ uint32_t q_sid[QW][QN], q_pix[QW][QN];   // sid | slot << 29, pixel
+    __shared__ int q_hit[QW][QN];
+    __shared__ T q_t[QW][QN], q_d[QW][3][QN];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
@@ -594,8 +650,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     if (lane < 4) g_kst[wave][lane] = 0;
 #endif
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    __shared__ IssueState s_is[4];
-    if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u};
+    if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u};
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
     uint32_t sid = 0, k = 0, slot = 0, pix = 0;
     bool live = false;
@@ -603,12 +658,13 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     int hit_i = -1;
     T hit_t = T(0);
     uint32_t slot_item = 0, slot_left = 0;   // lane s < kSlots: pixel item and unfinished samples of slot s
-    for (;;) {
-        // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
-        const uint32_t spp = cold_args<T>()->spp, depth = cold_args<T>()->depth;
-        bool fresh = false;
-        uint32_t frow = 0, fcol = 0;
-        unsigned long long freem = __ballot(!live);
+
+    // Hand the lanes of `want` new samples in rank order, opening pixel slots as needed; returns
+    // true in the lanes that got one.
+    auto issue = [&](unsigned long long want, uint32_t& i_sid, uint32_t& i_slot, uint32_t& i_pix,
+                     uint32_t& i_row, uint32_t& i_col) -> bool {
+        const uint32_t spp = cold_args<T>()->spp;
+        bool got = false;
         uint32_t busy = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
         uint32_t cur = __builtin_amdgcn_readfirstlane(s_is[wave].cur);
         uint32_t cur_next = __builtin_amdgcn_readfirstlane(s_is[wave].cur_next);
@@ -616,7 +672,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         uint32_t cur_row = __builtin_amdgcn_readfirstlane(s_is[wave].cur_row);
         uint32_t cur_col = __builtin_amdgcn_readfirstlane(s_is[wave].cur_col);
         bool drained = __builtin_amdgcn_readfirstlane(s_is[wave].drained) != 0u;
-        while (freem != 0ull && !drained) {
+        while (want != 0ull && !drained) {
             if (cur_next == spp) {
                 const uint32_t avail = ~busy & ((1u << kSlots) - 1u);
                 if (avail == 0u) break;   // every slot waits for straggler rays
@@ -635,55 +691,41 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 cur = s;
                 cur_next = 0;
             }
-            const bool isfree = (freem >> lane) & 1ull;
-            const uint32_t take = min((uint32_t)__popcll(freem), spp - cur_next);
-            const uint32_t r = (uint32_t)__popcll(freem & lt_mask);
-            const bool mine = isfree && r < take;
-            if (mine) { fresh = true; sid = cur_next + r; slot = cur; pix = cur_pix; frow = cur_row; fcol = cur_col; }
-            freem &= ~__ballot(mine);
+            const bool isw = (want >> lane) & 1ull;
+            const uint32_t take = min((uint32_t)__popcll(want), spp - cur_next);
+            const uint32_t r = (uint32_t)__popcll(want & lt_mask);
+            const bool mine = isw && r < take;
+            if (mine) { got = true; i_sid = cur_next + r; i_slot = cur; i_pix = cur_pix; i_row = cur_row; i_col = cur_col; }
+            want &= ~__ballot(mine);
             cur_next += take;
         }
-        if (lane == 0) s_is[wave] = IssueState{busy, cur, cur_next, cur_pix, cur_row, cur_col, drained ? 1u : 0u, 0u};
-        KSTAT(3, __ballot(fresh) != 0ull ? 1u : 0u);
-        // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
-        if (fresh || scat) next_ray<T, MODE == kModeScalar>(fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
-        if (fresh) {
-            k = 0;
-            live = true;
-            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
-        } else if (scat) {
-            k += 1u;
+        if (lane == 0) {
+            s_is[wave].busy = busy; s_is[wave].cur = cur; s_is[wave].cur_next = cur_next; s_is[wave].cur_pix = cur_pix;
+            s_is[wave].cur_row = cur_row; s_is[wave].cur_col = cur_col; s_is[wave].drained = drained ? 1u : 0u;
         }
-        if (__ballot(live) == 0ull) break;   // drained, and every slot finished
-        // ---- one sphere sweep for every live ray ----
-        const bool act = live && k < depth;
-        hit_i = -1;
-        if (act) hit_i = nearest_hit<T, ROOT2, MODE == kModeScalar>(p, o, d, hit_t);
-        const unsigned long long bact = __ballot(act);
-        if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
-        // ---- terminations: record e (and the colour of a sky hit) ----
-        const bool skyhit = act && hit_i < 0;
-        // A hit at the last bounce is not scattered: the ray stays enabled and reads black
-        // whatever its colour (ray_tracing.rs:495-497), and the scatter draws nothing observable.
-        const bool term = live && (!act || skyhit || k + 1 == depth);
-        scat = act && hit_i >= 0 && k + 1 < depth;
+        return got;
+    };
+
+    // Record this step's terminations (e: the bounce of a sky hit, or depth for a ray still
+    // enabled) and finish every pixel whose last sample this was.
+    auto terminate = [&](bool term, bool skyhit, uint32_t e, uint32_t t_slot, uint32_t t_sid, const V3<T>& tc,
+                         const V3<T>& td) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
-            sc.e(slot, sid) = skyhit ? k : depth;
+            sc.e(t_slot, t_sid) = e;
             if (MODE == kModeV2) {
-                if (skyhit) { sc.c(slot, 0, sid) = c.x; sc.c(slot, 1, sid) = c.y; sc.c(slot, 2, sid) = c.z; }
+                if (skyhit) { sc.c(t_slot, 0, t_sid) = tc.x; sc.c(t_slot, 1, t_sid) = tc.y; sc.c(t_slot, 2, t_sid) = tc.z; }
             } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
                 V3<T> v = mk(T(0.0), T(0.0), T(0.0));
-                if (skyhit) { const V3<T> sk = sky(d.y); v = mk(c.x * sk.x, c.y * sk.y, c.z * sk.z); }
-                sc.c(slot, 0, sid) = v.x; sc.c(slot, 1, sid) = v.y; sc.c(slot, 2, sid) = v.z;
+                if (skyhit) { const V3<T> sk = sky(td.y); v = mk(tc.x * sk.x, tc.y * sk.y, tc.z * sk.z); }
+                sc.c(t_slot, 0, t_sid) = v.x; sc.c(t_slot, 1, t_sid) = v.y; sc.c(t_slot, 2, t_sid) = v.z;
             }
         }
-        live = live && !term;
         unsigned long long tm = __ballot(term);
         bool synced = false;
         while (tm != 0ull) {
-            const uint32_t s = __builtin_amdgcn_readlane(slot, __builtin_ctzll(tm));
-            const unsigned long long m = __ballot(term && slot == s);
+            const uint32_t s = __builtin_amdgcn_readlane(t_slot, __builtin_ctzll(tm));
+            const unsigned long long m = __ballot(term && t_slot == s);
             tm &= ~m;
             if (lane == s) slot_left -= (uint32_t)__popcll(m);
             if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
@@ -695,6 +737,117 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
             }
         }
+    };
+
+    // CAMQ: one full-wave batch of primary rays.  Returns false when no sample could be issued.
+    auto camera_batch = [&]() -> bool {
+        uint32_t bsid = 0, bslot = 0, bpix = 0, brow = 0, bcol = 0;
+        const bool v = issue(~0ull, bsid, bslot, bpix, brow, bcol);
+        const unsigned long long vm = __ballot(v);
+        if (vm == 0ull) return false;
+        V3<T> bd = mk(T(0), T(0), T(0));
+        if (v) {   // Camera::get_ray (ray_tracing.rs:77-89) with origin == centre
+            const U4 r = [&] {
+                const auto& q0 = *cold_args<T>();
+                return philox(bsid, bpix, 0u, 0u, q0.k0, q0.k1);
+            }();
+            const auto& q = *cold_args_after<T>(r.a ^ r.b);
+            const T s1 = ((T)bcol + u01a(r, T(0))) / (T)q.W;
+            const T s2 = ((T)brow + u01b(r, T(0))) / (T)q.H;
+            const V3<T> vu = mk(q.vu[0], q.vu[1], q.vu[2]), vv = mk(q.vv[0], q.vv[1], q.vv[2]);
+            const V3<T> pc = add(mk(q.ulc[0], q.ulc[1], q.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
+            bd = unit(sub(pc, mk(q.center[0], q.center[1], q.center[2])));
+            if (MODE == kModeV2) wave_scratch<T>(wave).y(bslot, bsid) = bd.y;   // primary y (quirk Q2)
+        }
+        T bt = T(0);
+        int bi = -1;
+        if (v) bi = nearest_hit<T, ROOT2, SC, true>(p, bd, bd, bt);
+        if (lane == 0) { wcount[wave][0] += (uint32_t)__popcll(vm); wcount[wave][1] += 64u; }
+        const uint32_t depth = cold_args<T>()->depth;
+        const bool skyhit = v && bi < 0;
+        const bool term = v && (skyhit || depth == 1u);
+        const bool push = v && !term;
+        const unsigned long long pm = __ballot(push);
+        const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
+        const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
+        if (push) {
+            const uint32_t e = (qhead + qcount + (uint32_t)__popcll(pm & lt_mask)) % kQCap;
+            q_sid[wave][e] = bsid | (bslot << 29);
+            q_pix[wave][e] = bpix;
+            q_hit[wave][e] = bi;
+            q_t[wave][e] = bt;
+            q_d[wave][0][e] = bd.x; q_d[wave][1][e] = bd.y; q_d[wave][2][e] = bd.z;
+        }
+        if (lane == 0) s_is[wave].qcount = qcount + (uint32_t)__popcll(pm);
+        terminate(term, skyhit, skyhit ? 0u : depth, bslot, bsid, mk(T(1.0), T(1.0), T(1.0)), bd);
+        return true;
+    };
+
+    for (;;) {
+        bool fresh = false;
+        uint32_t frow = 0, fcol = 0;
+        if constexpr (CAMQ) {
+            // ---- top up the queue with camera batches, then free lanes pop primary-ray hits ----
+            const unsigned long long freem = __ballot(!live);
+            const uint32_t nfree = (uint32_t)__popcll(freem);
+            for (;;) {
+                const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
+                if (qcount >= nfree || qcount + 64u > kQCap) break;
+                if (!camera_batch()) break;
+            }
+            const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
+            const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
+            const uint32_t take = min(nfree, qcount);
+            const uint32_t r = (uint32_t)__popcll(freem & lt_mask);
+            if (!live && r < take) {
+                const uint32_t e = (qhead + r) % kQCap;
+                const uint32_t w0 = q_sid[wave][e];
+                sid = w0 & 0x1FFFFFFFu;
+                slot = w0 >> 29;
+                pix = q_pix[wave][e];
+                hit_i = q_hit[wave][e];
+                hit_t = q_t[wave][e];
+                d = mk(q_d[wave][0][e], q_d[wave][1][e], q_d[wave][2][e]);
+                const auto& q = *cold_args<T>();
+                o = mk(q.center[0], q.center[1], q.center[2]);
+                c = mk(T(1.0), T(1.0), T(1.0));
+                k = 0;
+                live = true;
+                scat = true;
+            }
+            if (lane == 0) { s_is[wave].qhead = (qhead + take) % kQCap; s_is[wave].qcount = qcount - take; }
+        } else {
+            // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
+            uint32_t nsid = 0, nslot = 0, npix = 0;
+            fresh = issue(__ballot(!live), nsid, nslot, npix, frow, fcol);
+            if (fresh) { sid = nsid; slot = nslot; pix = npix; }
+        }
+        KSTAT(3, __ballot(fresh) != 0ull ? 1u : 0u);
+        // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
+        if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
+        if (fresh) {
+            k = 0;
+            live = true;
+            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
+        } else if (scat) {
+            k += 1u;
+        }
+        if (__ballot(live) == 0ull) break;   // drained, and every slot finished
+        // ---- one sphere sweep for every live ray ----
+        const uint32_t depth = cold_args<T>()->depth;
+        const bool act = live && k < depth;
+        hit_i = -1;
+        if (act) hit_i = nearest_hit<T, ROOT2, SC>(p, o, d, hit_t);
+        const unsigned long long bact = __ballot(act);
+        if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
+        // ---- terminations: record e (and the colour of a sky hit) ----
+        const bool skyhit = act && hit_i < 0;
+        // A hit at the last bounce is not scattered: the ray stays enabled and reads black
+        // whatever its colour (ray_tracing.rs:495-497), and the scatter draws nothing observable.
+        const bool term = live && (!act || skyhit || k + 1 == depth);
+        scat = act && hit_i >= 0 && k + 1 < depth;
+        terminate(term, skyhit, skyhit ? k : depth, slot, sid, c, d);
+        live = live && !term;
     }
     if (lane == 0) {
         const auto& q = *cold_args<T>();
@@ -732,6 +885,7 @@ struct rt_context {
     bool have_first = false;
     // scene, fp64 and fp32 images
     void* sph64 = nullptr; void* sph32 = nullptr;   // grouped sphere records
+    void* cam64 = nullptr; void* cam32 = nullptr;   // camera-origin tables (same size; rebuilt per launch)
     void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
@@ -806,6 +960,8 @@ extern "C" int rt_context_create(int device, rt_context** out) {
 
 static void free_scene(rt_context* c) {
     (void)hipFree(c->sph64); (void)hipFree(c->sph32); (void)hipFree(c->mat64); (void)hipFree(c->mat32);
+    (void)hipFree(c->cam64); (void)hipFree(c->cam32);
+    c->cam64 = c->cam32 = nullptr;
     (void)hipFree(c->cen64); (void)hipFree(c->cen32);
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
@@ -892,6 +1048,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     int rc;
     if ((rc = up(&c->sph64, g64.data(), g64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->sph32, g32.data(), g32.size() * sizeof(float))) != RT_OK) return rc;
+    HIPCHK(hipMalloc(&c->cam64, g64.size() * sizeof(double)));
+    HIPCHK(hipMalloc(&c->cam32, g32.size() * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->cen32, c32.data(), c32.size() * sizeof(float))) != RT_OK) return rc;
     if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
@@ -910,6 +1068,20 @@ static bool check_range(const rt_camera* cam, const rt_tile_range* r) {
 }
 
 static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
+
+// The kernel instantiation for (flags, waves-per-SIMD target, camera batches).
+template <typename T, bool CAMQ>
+static void (*pick_kernel(uint32_t flags, int W))(KParams<T>) {
+    const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
+    constexpr int WM = kWavesModes<T>;
+    if (flags & RT_FLAG_MODE_SCALAR) return trace_paths<T, WM, false, kModeScalar, CAMQ>;
+    if (flags & RT_FLAG_MODE_VECTORIZED)
+        return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
+    if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
+    if (!CAMQ) return trace_paths<T, WM, false, kModeV2, false>;
+    return W >= 8 ? trace_paths<T, 8, false, kModeV2, true> : W >= 6 ? trace_paths<T, 6, false, kModeV2, true>
+         : W >= 5 ? trace_paths<T, 5, false, kModeV2, true> : trace_paths<T, 4, false, kModeV2, true>;
+}
 
 template <typename T>
 static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_t spp, uint64_t seed, uint32_t flags,
@@ -955,14 +1127,17 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // Minimum waves per SIMD the register allocation targets (RT_WAVES overrides; experiments).
     static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
     const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
-    const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
-    void (*kern)(KParams<T>);
-    if (flags & RT_FLAG_MODE_SCALAR) kern = trace_paths<T, kWavesRoot2, false, kModeScalar>;
-    else if (flags & RT_FLAG_MODE_VECTORIZED)
-        kern = r2 ? trace_paths<T, kWavesRoot2, true, kModeV1> : trace_paths<T, kWavesRoot2, false, kModeV1>;
-    else if (r2) kern = trace_paths<T, kWavesRoot2, true>;
-    else kern = W >= 8 ? trace_paths<T, 8, false> : W >= 6 ? trace_paths<T, 6, false> : W >= 5 ? trace_paths<T, 5, false>
-              : W >= 4 ? trace_paths<T, 4, false> : trace_paths<T, 1, false>;
+    // Camera batches + camera-origin table when every primary ray starts at the centre.
+    const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
+    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W) : pick_kernel<T, false>(flags, W);
+    if (camq) {
+        p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
+        const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>;
+        auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
+        hipLaunchKernelGGL(build, dim3((n_slots + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
+                           p.center[0], p.center[1], p.center[2]);
+        HIPCHK(hipGetLastError());
+    }
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));
     if (per_cu < 1) per_cu = 1;
