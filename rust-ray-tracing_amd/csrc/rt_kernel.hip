@@ -96,7 +96,7 @@ template <typename T> struct KParams {
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
-constexpr int kWavesF64 = 4;
+constexpr int kWavesF64 = 5;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 
