@@ -9,7 +9,7 @@ the RGB8 shards over RCCL and re-interleaves them (the north star's tiles + gath
 fixed as N grows -> "scaling": "strong").  Inputs (scene SoA, camera) are resident in HBM before
 the timed region.  Rank 0 prints one JSON line.
 
-roofline: the trace kernel is FP VALU-bound (no MFMA, ~0.03 B/sample of HBM traffic).
+roofline: the trace kernel is FP VALU-bound (no MFMA, ~0.09 B/sample of HBM traffic).
   algorithmic FLOP per launch = 17 * n_spheres * ray_segments   (segments counted
   in-kernel), achieved = that / average launch duration (HIP events on the launch stream).
 cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>) on this host's

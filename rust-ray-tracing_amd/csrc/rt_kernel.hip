@@ -7,20 +7,22 @@
 // reduction (ray_tracing.rs:486-504), /spp and Color::to_u8_array (renderer.rs:161,
 // color.rs:54-64).
 //
-// Mapping (one workgroup per pixel, wave64):
-//   * the pixel's spp samples are P = 4*ceil(spp/4) logical *positions* (the reference's
-//     C chunks x 4 lanes).  Active rays always occupy positions [0, n_k); position p lives
-//     on thread p % NT, slot p / NT, so n_k active rays occupy ceil(n_k/64) waves.
-//   * per bounce each active ray is traced against every sphere (sphere SoA read through
-//     the scalar cache: every lane of the wave tests the same sphere, operands in SGPRs);
-//   * survivors are compacted stably (the reference's shuffle, ray_tracing.rs:430-481) by
-//     __ballot + mbcnt + a cross-wave prefix over LDS counters, and their state moves to the
-//     new position in LDS, so the next bounce runs on dense waves;
-//   * quirk Q3 (the final read of buffer (C-1)%2, ray_tracing.rs:486) is reproduced without
-//     the second buffer: each position's final value is fixed at its retire bounce
-//     ("retire rule") and stored in an LDS array indexed by position; the
-//     final sum walks that array in the reference's order (per lane over chunks, then lanes),
-//     so fp64 results are bit-identical to the CPU restatement.
+// Mapping:
+//   * path regeneration: a persistent wave keeps one ray per lane from its camera ray to its
+//     termination, then takes the next sample (of this pixel or of the next one the wave pulls
+//     from an atomic counter; up to kSlots pixels in flight).  Every ray's bounce k depends only
+//     on its own state and the counter-based RNG key (sample, pixel, k, stream), so no ray waits
+//     for the others; lane utilisation is ~1.0.
+//   * each sweep tests every live ray against every sphere: spheres stream through the scalar
+//     cache in 64-byte groups (s_load_dwordx16 into SGPRs, a free broadcast to all 64 lanes),
+//     two spheres per packed-FP32 instruction, one branch per group on a sign-bit filter.
+//   * pinhole cameras: primary rays run in full-wave camera batches against a per-launch
+//     camera-origin table (oc and c are the same for every primary ray), hits wait in an LDS
+//     queue for free lanes.
+//   * the reference's positions (its per-bounce stable shuffle) are a function of the per-sample
+//     termination bounces alone; when a pixel's last sample ends, finish_pixel replays them,
+//     applies quirk Q3's buffer read ("retire rule") and sums in the reference's order, so fp64
+//     and fp32 results are bit-identical to the CPU restatement in oracle/.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
