@@ -445,7 +445,10 @@ __device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(
 // retire rule and sums in the reference's order — the same values, bit for bit,
 // as the bounce-synchronous schedule, with every lane busy and no per-bounce ray-state traffic.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kSlots = 8;   // pixels a wave may have in flight (lane s holds slot s's metadata)
+#ifndef RT_EXP_SLOTS
+#define RT_EXP_SLOTS 8
+#endif
+constexpr uint32_t kSlots = RT_EXP_SLOTS;   // pixels a wave may have in flight (lane s holds slot s's metadata)
 
 // Semantics modes (RT_FLAG_MODE_*): which of the reference's renderers the kernel reproduces.
 enum Mode : int {
