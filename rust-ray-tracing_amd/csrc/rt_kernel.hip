@@ -449,6 +449,7 @@ __device__ __forceinline__ void wave_mem_sync() { asm volatile("s_waitcnt vmcnt(
 #define RT_EXP_SLOTS 8
 #endif
 constexpr uint32_t kSlots = RT_EXP_SLOTS;   // pixels a wave may have in flight (lane s holds slot s's metadata)
+static_assert(kSlots >= 1 && kSlots <= 8, "the camera-batch queue packs the slot into 3 bits (sid | slot << 29)");
 
 // Semantics modes (RT_FLAG_MODE_*): which of the reference's renderers the kernel reproduces.
 enum Mode : int {
