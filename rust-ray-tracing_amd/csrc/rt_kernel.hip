@@ -531,7 +531,11 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     }
     wave_mem_sync();
     uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
+#ifdef RT_EXP_SKIP_REPLAY
+    for (uint32_t k = 0; k < 0u; ++k) {   // timing experiment only: results are wrong
+#else
     for (uint32_t k = 0; k < (MODE == kModeV2 ? K : 0u); ++k) {
+#endif
         if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
             kb = k;
             hist[lane] = 0;
@@ -559,11 +563,16 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                     const uint32_t pold = cge + (uint32_t)__popcll(bge & lt_mask);
                     const uint32_t pnew = n_next + ceq + (uint32_t)__popcll(beq & lt_mask);
                     const V3<T> c = mk(sc.c(s, 0, i), sc.c(s, 1, i), sc.c(s, 2, i));
-                    if (U && pold >= lo && pold < hi) {
-                        const V3<T> sk = sky(sc.y(s, pold));
-                        sc.v(0, pold) = c.x * sk.x; sc.v(1, pold) = c.y * sk.y; sc.v(2, pold) = c.z * sk.z;
+                    const bool w_old = U && pold >= lo && pold < hi;
+                    const bool w_new = !U || pnew < lo || pnew >= hi;
+                    // At most one write except when the old position retires now and the new one
+                    // later: one sky evaluation for the common case, a second only for that one.
+                    if (w_old || w_new) {
+                        const uint32_t q1 = w_old ? pold : pnew;
+                        const V3<T> sk = sky(sc.y(s, q1));
+                        sc.v(0, q1) = c.x * sk.x; sc.v(1, q1) = c.y * sk.y; sc.v(2, q1) = c.z * sk.z;
                     }
-                    if (!U || pnew < lo || pnew >= hi) {
+                    if (w_old && w_new) {
                         const V3<T> sk = sky(sc.y(s, pnew));
                         sc.v(0, pnew) = c.x * sk.x; sc.v(1, pnew) = c.y * sk.y; sc.v(2, pnew) = c.z * sk.z;
                     }

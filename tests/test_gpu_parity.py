@@ -354,3 +354,15 @@ def test_negative_zero_camera_centre(renderer, scene_100, prec):
     cam = _cam(24, 14, center=(-0.0, 2.0, 18.5), look_at=(0.0, 0.0, 0.0))
     assert cam.center[0] == 0.0 and math.copysign(1.0, cam.center[0]) < 0
     assert_parity(renderer, scene_100, cam, 50, 12, prec)
+
+
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_ROOT2, abi.RT_FLAG_MODE_SCALAR,
+                                   abi.RT_FLAG_MODE_SCALAR | abi.RT_FLAG_F32, abi.RT_FLAG_ROOT2 | abi.RT_FLAG_F32])
+def test_every_primary_ray_hits(renderer, flags):
+    """Camera inside a big sphere with both roots allowed: every primary ray hits, so each camera
+    batch pushes 64 queue entries and the per-wave queue runs full (the top-up stops at 64 free
+    slots).  A small sphere inside adds a second, nearer candidate for some rays."""
+    mats = [rt.Lambertian((0.6, 0.5, 0.4)), rt.Metal((0.9, 0.9, 0.9), 0.2)]
+    flat = rt.FlatScene(np.array([[16.0, 2.0, 18.5], [0.0, 0.0, 0.0]]), np.array([60.0, 3.0]),
+                        np.array([0, 1], np.uint32), mats)
+    assert_parity(renderer, flat, cam_for(32, 18), 12, 64, flags)
