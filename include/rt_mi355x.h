@@ -132,7 +132,9 @@ int rt_context_destroy(rt_context* ctx);
 int rt_context_set_scene(rt_context* ctx, const rt_scene* scene);
 /* Enqueue one render on `stream` (a hipStream_t; NULL = the HIP null stream, as in every HIP
  * API).  d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous.  Renders on
- * one context must be issued to one stream at a time (they share the context's work counter). */
+ * one context share its work counter, scratch and camera table: a render on a different stream
+ * than the previous one first synchronises the previous stream, so they never overlap.  Use one
+ * context per concurrent stream for overlap. */
 int rt_render_async(rt_context* ctx, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
                     uint64_t seed, uint32_t flags, const rt_tile_range* range, void* d_rgb8,
                     void* d_linear, void* stream);

@@ -909,6 +909,8 @@ struct rt_context {
     size_t scratch_bytes = 0;
     int n_cu = 0;
     uint64_t samples = 0, pixels = 0;
+    hipStream_t last_stream = nullptr;   // stream of the previous render (they share scratch and tables)
+    bool have_last = false;
 };
 
 extern "C" const char* rt_last_error(void) { return g_err.c_str(); }
@@ -1199,6 +1201,11 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
     const bool f32 = (flags & RT_FLAG_F32) != 0;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t st = (hipStream_t)stream;   // NULL = the HIP null stream
+    // Renders on one context share its work counter, scratch and camera table: a render on a new
+    // stream first waits for the previous stream, so cross-stream use serialises instead of racing.
+    if (c->have_last && c->last_stream != st) HIPCHK(hipStreamSynchronize(c->last_stream));
+    c->last_stream = st;
+    c->have_last = true;
     if (!c->have_first) {
         HIPCHK(hipEventRecord(c->ev_first, st));
         c->have_first = true;
