@@ -366,3 +366,42 @@ def test_every_primary_ray_hits(renderer, flags):
     flat = rt.FlatScene(np.array([[16.0, 2.0, 18.5], [0.0, 0.0, 0.0]]), np.array([60.0, 3.0]),
                         np.array([0, 1], np.uint32), mats)
     assert_parity(renderer, flat, cam_for(32, 18), 12, 64, flags)
+
+
+def test_one_context_two_streams(renderer, scene_100):
+    """Renders on one context issued to two different streams without any host sync in between:
+    the second waits for the first (shared counter, scratch and camera table), so both images
+    equal single renders.  Streams come from the HIP runtime the library already loaded."""
+    lib = renderer.lib
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    cam = cam_for(40, 24)
+    renderer.set_scene(scene_100)
+    npx = 40 * 24
+    want = {}
+    for seed in (11, 22):
+        renderer.seed = seed
+        renderer.flags = abi.RT_FLAG_F32
+        want[seed] = renderer.render_flat(50, 32, scene_100, cam, want_linear=True)[1]
+    streams = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for st in streams:
+        assert hip.hipStreamCreate(ctypes.byref(st)) == 0
+    bufs = [ctypes.c_void_p(), ctypes.c_void_p()]
+    for b in bufs:
+        abi.check(lib, lib.rt_device_alloc(renderer.ctx, npx * 3 * 8, ctypes.byref(b)))
+    try:
+        tr = abi.RtTileRange(0, 1, 24, 0, 40)
+        for seed, st, b in zip((11, 22), streams, bufs):
+            abi.check(lib, lib.rt_render_async(renderer.ctx, ctypes.byref(cam), 50, 32, seed, abi.RT_FLAG_F32,
+                                               ctypes.byref(tr), None, b, st))
+        stats = abi.RtStats()
+        abi.check(lib, lib.rt_context_collect(renderer.ctx, streams[1], ctypes.byref(stats)))
+        for seed, b in zip((11, 22), bufs):
+            got = np.empty((npx, 3), dtype=np.float64)
+            abi.check(lib, lib.rt_memcpy_d2h(renderer.ctx, got.ctypes.data, b, npx * 3 * 8))
+            np.testing.assert_array_equal(got, want[seed])
+        assert stats.samples == 2 * npx * 32
+    finally:
+        for b in bufs:
+            lib.rt_device_free(renderer.ctx, b)
+        for st in streams:
+            hip.hipStreamDestroy(st)
