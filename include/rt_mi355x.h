@@ -126,23 +126,28 @@ int rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t max_bounc
 /* ---- device-resident API: scene kept in HBM across calls, outputs in device memory ---- */
 typedef struct rt_context rt_context;
 
+/* The renderer object: TileRenderer::new (renderer.rs:232-241) and its drop; one per GPU. */
 int rt_context_create(int device, rt_context** out);
 int rt_context_destroy(rt_context* ctx);
-/* Upload (replace) the scene; copies fp64 and fp32 SoA images into HBM. */
+/* Upload (replace) the scene, the Arc<Scene> handed to Renderer::render (main.rs:43,
+ * renderer.rs:38-40); copies fp64 and fp32 SoA images into HBM. */
 int rt_context_set_scene(rt_context* ctx, const rt_scene* scene);
 /* Enqueue one render on `stream` (a hipStream_t; NULL = the HIP null stream, as in every HIP
- * API).  d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous.  Renders on
+ * API): the pixels of `range` through TileRenderTask::render_vectorized2 (renderer.rs:141-176),
+ * i.e. one share of TileRenderer::render's tile loop (renderer.rs:248-296).  d_rgb8 / d_linear are device pointers (either may be NULL).  Asynchronous.  Renders on
  * one context share its work counter, scratch and camera table: a render on a different stream
  * than the previous one first synchronises the previous stream, so they never overlap.  Use one
  * context per concurrent stream for overlap. */
 int rt_render_async(rt_context* ctx, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
                     uint64_t seed, uint32_t flags, const rt_tile_range* range, void* d_rgb8,
                     void* d_linear, void* stream);
-/* Synchronise `stream` (NULL = null stream), then report and reset the counters accumulated by the renders
+/* RenderStat (renderer.rs:11-34) for the renders since the last call.
+ * Synchronise `stream` (NULL = null stream), then report and reset the counters accumulated by the renders
  * enqueued since the last call (ray_segments, error flag).  kernel_ms = device time between
  * the first and last enqueued render (HIP events on that stream). */
 int rt_context_collect(rt_context* ctx, void* stream, rt_stats* stats);
-/* Device memory helpers (so hosts without a HIP toolchain can drive the async API). */
+/* Device memory helpers (so hosts without a HIP toolchain can drive the async API); no reference
+ * counterpart (the reference has no device memory). */
 int rt_device_alloc(rt_context* ctx, size_t bytes, void** out);
 int rt_device_free(rt_context* ctx, void* ptr);
 int rt_memcpy_d2h(rt_context* ctx, void* dst, const void* src, size_t bytes);   /* synchronises the device */
