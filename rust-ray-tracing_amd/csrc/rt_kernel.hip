@@ -29,6 +29,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <limits>
@@ -56,6 +57,9 @@ template <typename T> struct MatT {
 //         so each quantity of a sphere pair is an adjacent SGPR pair for packed-FP32 VALU ops;
 //   fp64: 2 spheres per group as {cx, cy, cz, r^2}.
 // A separate AoS table {cx, cy, cz, r^2} per sphere serves the per-lane finalize gather.
+// The filter stream (both precisions) is fp32 in the fp32 layout, with r^2 replaced by the filter's
+// r2f: r^2 rounded up to fp32, +inf for "always exact" spheres, -inf for dummies (see
+// general_sweep).
 template <typename T> constexpr uint32_t kGroup = 64 / (4 * sizeof(T));
 template <typename T> struct alignas(64) SphGroup { T v[64 / sizeof(T)]; };
 
@@ -93,6 +97,9 @@ template <typename T> struct KParams {
     size_t scratch_stride;
     uint32_t vbytes, sbytes;   // trace_paths: value-array bytes, per-slot record bytes (PScratch)
     const T* camsph;           // camera-origin table {oc, c} in the sph layout (pinhole launches)
+    const float* fsph;         // filter stream: fp32 groups of 4 {cx, cy, cz, r2f} (layout above)
+    uint32_t n_fgroups;
+    float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
 };
 
 constexpr int kSegShards = 256;
@@ -101,6 +108,8 @@ constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured s
 constexpr int kWavesF64 = 5;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
+constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
+constexpr double kExactRatio = 8.0;  // spheres with |c|_1 + r > kExactRatio x the median are "always exact"
 
 // Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..6.
 #ifdef RT_KSTATS
@@ -162,6 +171,43 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
     if (g < ng) group(A, g);
 }
 
+// The general-sweep filter for one 4-sphere group (nearest_hit): per sphere pair
+//   x = cx*e1x + (cz*e1z - oe1),  y = cx*e2x + (cy*e2y + (cz*e2z - oe2)),  D = (r2f + m - y^2) - x^2
+// in packed FP32 (two spheres per op), then acc = ~(D0 & D1 & D2 & D3) on the sign bits.  The
+// per-lane constants come two to a VGPR pair, K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, m},
+// K3 = {-oe1, -oe2}, and each use broadcasts one half with op_sel / op_sel_hi (the compiler
+// materialises such splats as extra VGPR pairs).  The two pairs are interleaved so that no packed
+// result is read by the next instruction (the one-wait-state packed-FP32 read hazard the compiler
+// pads with s_nop).  16 packed ops, then v_and3 + v_bitop3 on the sign bits.
+__device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3) {
+    const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
+    const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
+    f2 a0, b0, a1, b1, r0, r1;
+    asm volatile(
+        "v_pk_fma_f32 %[a0], %[cz0], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"   // cz*e1z - oe1
+        "v_pk_fma_f32 %[b0], %[cz0], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"   // cz*e2z - oe2
+        "v_pk_fma_f32 %[a1], %[cz1], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
+        "v_pk_fma_f32 %[b1], %[cz1], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[a0], %[cx0], %[K0], %[a0] op_sel_hi:[1,0,1]\n\t"                  // x = cx*e1x + .
+        "v_pk_fma_f32 %[b0], %[cy0], %[K1], %[b0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"   // cy*e2y + .
+        "v_pk_fma_f32 %[a1], %[cx1], %[K0], %[a1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b1], %[cy1], %[K1], %[b1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_add_f32 %[r0], %[rr0], %[K2] op_sel:[0,1] op_sel_hi:[1,1]\n\t"              // r2f + m
+        "v_pk_fma_f32 %[b0], %[cx0], %[K1], %[b0] op_sel_hi:[1,0,1]\n\t"                  // y = cx*e2x + .
+        "v_pk_add_f32 %[r1], %[rr1], %[K2] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
+        "v_pk_fma_f32 %[b1], %[cx1], %[K1], %[b1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[r0], %[b0], %[b0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"       // - y^2
+        "v_pk_fma_f32 %[r1], %[b1], %[b1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[r0], %[a0], %[a0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"       // D = . - x^2
+        "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+        : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
+        : [cx0] "s"(cx0), [cy0] "s"(cy0), [cz0] "s"(cz0), [rr0] "s"(rr0), [cx1] "s"(cx1), [cy1] "s"(cy1),
+          [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3));
+    // ~(D0 & D1 & D2 & D3): sign set iff some sphere of the group passes (D >= +0)
+    const uint32_t t = __float_as_uint(r0.x) & __float_as_uint(r0.y) & __float_as_uint(r1.x);
+    return __builtin_amdgcn_bitop3_b32(t, __float_as_uint(r1.y), 0u, 0x3F);
+}
+
 // The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
 // index of the nearest valid hit (-1: the sky, :421-424) and its t.
 // SCALAR selects Sphere::hit + Scene::hit (objects.rs:216-247, ray_tracing.rs:231-235): no FMA,
@@ -178,8 +224,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     // Sphere::hit_packed (objects.rs:249-290) + PackedHitRecords::update (objects.rs:140-155)
     // for a candidate whose discriminant is non-negative.  Exact pre-filter: with hb >= 0,
     // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
+    KSTAT(CAMT ? 3 : 1);   // sweeps (one per wave)
     auto hit = [&](T hb, T disc, uint32_t i) {
-        KSTAT(1);
         if constexpr (SCALAR) {   // objects.rs:227-234 and min_by_key (first minimum)
             const T sd = sqrt(disc);
             T root = (-hb - sd) / a;
@@ -205,39 +251,31 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
     // Read through the laundered kernarg pointer at each sweep, so the sphere pointer and count do
     // not hold SGPRs across the persistent loop (they were spilled to VGPR lanes, 2 VALU a group).
-    const auto& qa = *cold_args<T>();
-    cptr<T> f = (cptr<T>)__builtin_assume_aligned(CAMT ? qa.camsph : qa.sph, 64);
-    const uint32_t ng = qa.n_groups;
-    // Candidate filter, branch-free, on sign bits: a sphere can only be hit if disc >= +0 (disc is
-    // never -0: fma(hb, hb, -(a*c)) and hb*hb - a*c round an exact zero to +0; NaNs never give a
-    // valid root), so ~(bits(d0) & bits(d1) & ...) has its sign set iff some sphere of the group
-    // may be a candidate: one v_and3 + one v_bitop3 + one compare per 64-byte group (fp32).
-    // Testing hb's sign too (root1 needs hb < 0 under Q1) would drop the spheres behind the ray
-    // but costs two more VALU on every group; a same-box A/B measured the disc-only filter 1.8 %
-    // (fp32) / 0.8 % (fp64) faster.  Inside a taken group, cand_f re-tests each
-    // sphere (a float superset of the exact test) and hit() decides exactly, so the filter never
-    // changes a result.
     auto sbits = [](T x) -> uint32_t {
         if constexpr (sizeof(T) == 4) return __float_as_uint(x);
         else return (uint32_t)__double2hiint(x);
     };
     constexpr bool kBothRoots = root2 || SCALAR;
     auto is_cand = [](uint32_t m) -> bool { return (int32_t)m < 0; };
-    // Per-sphere test inside a taken group: a float superset of cand (hb == +0 passes too), so the
-    // group test can fold the four sign words into one chain of v_bitop3.
+    // Per-sphere test inside a taken group: a float superset of cand (hb == +0 passes too).
     auto cand_f = [&](T hb, T disc) -> bool { return kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)); };
-    if constexpr (sizeof(T) == 4) {
-        // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two spheres,
-        // so the results are bit-identical to the scalar sequence (:252-257).
-        const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
-        const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
-        const f2 na = {-a, -a};
-        auto group = [&](const SphGroup<T>& cur, uint32_t g) {
-            f2 hb[2], disc[2];
+    if constexpr (CAMT) {
+        // Camera batches: {ocx, ocy, ocz, c} from the camera-origin table, so the exact test is
+        // hb (3 ops) and disc (2).  Filter on the exact sign bits: a sphere can only be hit if
+        // disc >= +0 (disc is never -0: fma(hb, hb, -(a*c)) and hb*hb - a*c round an exact zero
+        // to +0; NaNs never give a valid root), so ~(bits(d0) & bits(d1) & ...) has its sign set
+        // iff some sphere of the group may be a candidate (v_and3 + v_bitop3 + one compare).
+        const auto& qa = *cold_args<T>();
+        cptr<T> f = (cptr<T>)__builtin_assume_aligned(qa.camsph, 64);
+        const uint32_t ng = qa.n_groups;
+        if constexpr (sizeof(T) == 4) {
+            const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+            const f2 na = {-a, -a};
+            auto group = [&](const SphGroup<T>& cur, uint32_t g) {
+                f2 hb[2], disc[2];
 #pragma unroll
-            for (uint32_t q = 0; q < 2; ++q) {
-                const T* v = &cur.v[8 * q];
-                if constexpr (CAMT) {   // {ocx, ocy, ocz, c} pairs from the camera-origin table
+                for (uint32_t q = 0; q < 2; ++q) {
+                    const T* v = &cur.v[8 * q];
                     const f2 ocx = {v[0], v[1]}, ocy = {v[2], v[3]}, ocz = {v[4], v[5]}, c = {v[6], v[7]};
                     if constexpr (SCALAR) {
                         hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
@@ -246,67 +284,140 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));
                         disc[q] = fma2(hb[q], hb[q], na * c);
                     }
-                    continue;
                 }
-                const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
-                const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
-                if constexpr (SCALAR) {                                           // objects.rs:217-222
-                    hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
-                    const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
-                    disc[q] = hb[q] * hb[q] - (-na) * c;
-                } else {
-                    hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));               // :255
-                    const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;  // :256
-                    disc[q] = fma2(hb[q], hb[q], na * c);                         // :257
+                const uint32_t t = sbits(disc[0].x) & sbits(disc[0].y) & sbits(disc[1].x);   // v_and3_b32
+                const uint32_t acc = __builtin_amdgcn_bitop3_b32(t, sbits(disc[1].y), 0u, 0x3F);   // ~(S0 & S1)
+                if (is_cand(acc)) {
+                    KSTAT(2);
+                    const uint32_t i0 = 4 * g;
+                    if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, i0);
+                    if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, i0 + 1);
+                    if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, i0 + 2);
+                    if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, i0 + 3);
                 }
-            }
-            // acc = cand0 | cand1 | cand2 | cand3 as a strict chain: v_bitop3 computes
-            // S0 | (~S1 & S2) (table 0xF2) in one op, so the group test is 4 VALU + 1 compare.
-            // ~(d0 & d1 & d2 & d3): sign set iff some disc >= +0
-            const uint32_t t = sbits(disc[0].x) & sbits(disc[0].y) & sbits(disc[1].x);   // v_and3_b32
-            const uint32_t acc = __builtin_amdgcn_bitop3_b32(t, sbits(disc[1].y), 0u, 0x3F);   // ~(S0 & S1)
-            if (is_cand(acc)) {
-                KSTAT(0);
-                KSTAT(2, (uint32_t)__popcll(__ballot(cand_f(hb[0].x, disc[0].x))) + (uint32_t)__popcll(__ballot(cand_f(hb[0].y, disc[0].y))) +
-                         (uint32_t)__popcll(__ballot(cand_f(hb[1].x, disc[1].x))) + (uint32_t)__popcll(__ballot(cand_f(hb[1].y, disc[1].y))));
+            };
+            sphere_loop(f, ng, group);
+        } else {
+            auto group = [&](const SphGroup<T>& cur, uint32_t g) {
+                T hb[2], disc[2];
+#pragma unroll
+                for (uint32_t j = 0; j < 2; ++j) {
+                    const T* v = &cur.v[4 * j];
+                    const V3<T> oc = mk(v[0], v[1], v[2]);
+                    hb[j] = SCALAR ? dot(oc, d) : pk_dot(oc, d);
+                    disc[j] = SCALAR ? hb[j] * hb[j] - a * v[3] : fma(hb[j], hb[j], -a * v[3]);
+                }
+                const uint32_t acc = __builtin_amdgcn_bitop3_b32(sbits(disc[0]), sbits(disc[1]), 0u, 0x3F);   // ~(d0 & d1)
+                if (is_cand(acc)) {
+                    KSTAT(2);
+                    if (cand_f(hb[0], disc[0])) hit(hb[0], disc[0], 2 * g);
+                    if (cand_f(hb[1], disc[1])) hit(hb[1], disc[1], 2 * g + 1);
+                }
+            };
+            sphere_loop(f, ng, group);
+        }
+    } else {
+        // General sweep: a conservative fp32 distance filter, then the exact test for taken groups.
+        //
+        // Filter: with e1, e2 an orthonormal basis of the plane perpendicular to d (e1 has no y
+        // component), x = (c - o).e1 and y = (c - o).e2 are the centre's offset from the ray's
+        // line, so the line meets the sphere iff x^2 + y^2 <= r^2.  Per sphere pair that is
+        // x: 2 packed FMAs, y: 3, r2f + m: 1, D = r2f + m - x^2 - y^2: 2 -- 8 ops against the
+        // exact test's 12.  The margin m = 48 u ((max|c|_1 + |o|_1)^2 + max r2f), u = 2^-24,
+        // covers the reference's own rounding of disc (a sphere it computes disc >= 0 for may lie
+        // slightly outside), the filter's basis and rounding errors, and for fp64 rays the
+        // conversion to fp32: a first-order bound is ~30 u, 80M adversarial
+        // near-tangent cases need at most 5 u (tests/test_filter_margin.py).  So every sphere the
+        // reference could hit passes; a group with any passing sphere recomputes all four exactly
+        // from the exact stream, and only the exact values ever reach hit().
+        // Spheres far outside the scene (|c|_1 + r > 8x the median, e.g. a ground sphere) would
+        // inflate the margin for all: the host gives them r2f = +inf, "always exact".  Lanes whose
+        // basis degenerates (d nearly parallel to y) or whose origin is huge get m = +inf and a
+        // zero basis, so every group is taken for them (D = +inf, or a positive default NaN for a
+        // -inf dummy, which only costs an exact test).  RT_FILTER_OFF=1 (host, diagnostics and
+        // tests) sets f_cmax = +inf: every lane degenerate, every group exact.
+        const auto& qa = *cold_args<T>();
+        cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.fsph, 64);
+        cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
+        const uint32_t ngf = qa.n_fgroups;
+        const float fdx = (float)d.x, fdy = (float)d.y, fdz = (float)d.z;
+        const float fox = (float)o.x, foy = (float)o.y, foz = (float)o.z;
+        const float L = __builtin_fmaf(fdz, fdz, fdx * fdx);
+        const float af = __builtin_fmaf(fdz, fdz, __builtin_fmaf(fdy, fdy, fdx * fdx));
+        const float s1 = 1.0f / sqrtf(L), s2 = 1.0f / sqrtf(L * af);
+        float e1x = fdz * s1, e1z = -fdx * s1;
+        float e2x = -(fdx * fdy) * s2, e2y = L * s2, e2z = -(fdy * fdz) * s2;
+        float oe1 = __builtin_fmaf(foz, e1z, fox * e1x);
+        float oe2 = __builtin_fmaf(foz, e2z, __builtin_fmaf(foy, e2y, fox * e2x));
+        const float on = fabsf(fox) + fabsf(foy) + fabsf(foz);
+        const float pm = qa.f_cmax + on;
+        float m = kFilterMargin * __builtin_fmaf(pm, pm, qa.f_r2max);
+        // Degenerate lanes: L*af must not underflow (L >= 1e-15: d within ~3e-8 of the y axis), and
+        // x^2, y^2 must stay finite (|c|_1 + |o|_1 <= 1e15), so D is never inf - inf.
+        if (!(L >= 1e-15f) || !(pm <= 1e15f)) {
+            e1x = e1z = e2x = e2y = e2z = 0.0f;
+            oe1 = oe2 = 0.0f;
+            m = INFINITY;
+        }
+        // Two per-lane constants per VGPR pair; every use broadcasts one half through the packed
+        // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
+        const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, m}, K3 = {-oe1, -oe2};
+        // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222).
+        auto exact4 = [&](uint32_t g) {
+            KSTAT(0);
+            if constexpr (sizeof(T) == 4) {
+                // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two
+                // spheres, so the results are bit-identical to the scalar sequence (:252-257).
+                const SphGroup<T> cur = load_group(fe, g);
+                const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+                const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+                const f2 na = {-a, -a};
+                f2 hb[2], disc[2];
+#pragma unroll
+                for (uint32_t q = 0; q < 2; ++q) {
+                    const T* v = &cur.v[8 * q];
+                    const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
+                    const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
+                    if constexpr (SCALAR) {                                           // objects.rs:217-222
+                        hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
+                        const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+                        disc[q] = hb[q] * hb[q] - (-na) * c;
+                    } else {
+                        hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));               // :255
+                        const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;  // :256
+                        disc[q] = fma2(hb[q], hb[q], na * c);                         // :257
+                    }
+                }
                 const uint32_t i0 = 4 * g;
                 if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, i0);
                 if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, i0 + 1);
                 if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, i0 + 2);
                 if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, i0 + 3);
-            }
-        };
-        sphere_loop(f, ng, group);
-    } else {
-        auto group = [&](const SphGroup<T>& cur, uint32_t g) {
-            T hb[2], disc[2];
+            } else {
+                const SphGroup<T> c0 = load_group(fe, 2 * g), c1 = load_group(fe, 2 * g + 1);
+                T hb[4], disc[4];
 #pragma unroll
-            for (uint32_t j = 0; j < 2; ++j) {
-                const T* v = &cur.v[4 * j];
-                if constexpr (CAMT) {   // {ocx, ocy, ocz, c} from the camera-origin table
-                    const V3<T> oc = mk(v[0], v[1], v[2]);
-                    hb[j] = SCALAR ? dot(oc, d) : pk_dot(oc, d);
-                    disc[j] = SCALAR ? hb[j] * hb[j] - a * v[3] : fma(hb[j], hb[j], -a * v[3]);
-                    continue;
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const T* v = j < 2 ? &c0.v[4 * j] : &c1.v[4 * (j - 2)];
+                    const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
+                    if constexpr (SCALAR) {                                    // objects.rs:217-222
+                        hb[j] = dot(oc, d);
+                        disc[j] = hb[j] * hb[j] - a * (len2(oc) - v[3]);
+                    } else {
+                        hb[j] = pk_dot(oc, d);                                 // :255
+                        const T c = pk_len2(oc) - v[3];                        // :256
+                        disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
+                    }
                 }
-                const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
-                if constexpr (SCALAR) {                                    // objects.rs:217-222
-                    hb[j] = dot(oc, d);
-                    disc[j] = hb[j] * hb[j] - a * (len2(oc) - v[3]);
-                } else {
-                    hb[j] = pk_dot(oc, d);                                 // :255
-                    const T c = pk_len2(oc) - v[3];                        // :256
-                    disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
-                }
-            }
-            // ~(d0 & d1): sign set iff some disc >= +0
-            const uint32_t acc = __builtin_amdgcn_bitop3_b32(sbits(disc[0]), sbits(disc[1]), 0u, 0x3F);
-            if (is_cand(acc)) {
-                if (cand_f(hb[0], disc[0])) hit(hb[0], disc[0], 2 * g);
-                if (cand_f(hb[1], disc[1])) hit(hb[1], disc[1], 2 * g + 1);
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (cand_f(hb[j], disc[j])) hit(hb[j], disc[j], 4 * g + j);
             }
         };
-        sphere_loop(f, ng, group);
+        auto group = [&](const SphGroup<float>& cur, uint32_t g) {
+            if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g);
+        };
+        sphere_loop(ff, ngf, group);
     }
     t_out = best_t;
     return best;
@@ -833,7 +944,6 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             fresh = issue(__ballot(!live), nsid, nslot, npix, frow, fcol);
             if (fresh) { sid = nsid; slot = nslot; pix = npix; }
         }
-        KSTAT(3, __ballot(fresh) != 0ull ? 1u : 0u);
         // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
         if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
         if (fresh) {
@@ -896,6 +1006,9 @@ struct rt_context {
     bool have_first = false;
     // scene, fp64 and fp32 images
     void* sph64 = nullptr; void* sph32 = nullptr;   // grouped sphere records
+    void* fsph64 = nullptr; void* fsph32 = nullptr; // fp32 filter streams (for fp64 / fp32 rays)
+    uint32_t n_fgroups = 0;
+    float f_cmax64 = 0, f_r2max64 = 0, f_cmax32 = 0, f_r2max32 = 0;
     void* cam64 = nullptr; void* cam32 = nullptr;   // camera-origin tables (same size; rebuilt per launch)
     void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
     uint32_t n_groups64 = 0, n_groups32 = 0;
@@ -975,6 +1088,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->sph64); (void)hipFree(c->sph32); (void)hipFree(c->mat64); (void)hipFree(c->mat32);
     (void)hipFree(c->cam64); (void)hipFree(c->cam32);
     c->cam64 = c->cam32 = nullptr;
+    (void)hipFree(c->fsph64); (void)hipFree(c->fsph32);
+    c->fsph64 = c->fsph32 = nullptr;
     (void)hipFree(c->cen64); (void)hipFree(c->cen32);
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
@@ -1034,6 +1149,53 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
     }
 }
 
+// Filter stream for rays in precision T (layout at SphGroup, fp32, 4 spheres per group): centres
+// as the T kernel sees them, converted to fp32; r2f = the kernel's r^2 (r.powi(2) in T) rounded up
+// to fp32; +inf for "always exact" spheres; -inf for dummies.  Returns the margin bounds over the
+// other spheres: max |c|_1 (rounded up) and max r2f.
+template <typename T>
+static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float>& grp, uint32_t& n_fgroups,
+                        float& cmax, float& r2max) {
+    n_fgroups = (n + 3) / 4;
+    std::vector<double> key(n);
+    for (uint32_t i = 0; i < n; ++i)
+        key[i] = std::fabs((double)cen[4 * i]) + std::fabs((double)cen[4 * i + 1]) + std::fabs((double)cen[4 * i + 2]) +
+                 std::fabs((double)cen[4 * i + 3]);
+    double median = 0.0;
+    if (n) {
+        std::vector<double> k2 = key;
+        std::nth_element(k2.begin(), k2.begin() + n / 2, k2.end());
+        median = k2[n / 2];
+    }
+    auto up32 = [](double v) -> float {   // fp32 >= v
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+        return f;
+    };
+    double cm = 0.0, rm = 0.0;
+    grp.assign((size_t)16 * (n_fgroups + 1), 0.0f);
+    for (uint32_t i = 0; i < 4 * (n_fgroups + 1); ++i) {
+        float f[4] = {0.0f, 0.0f, 0.0f, -std::numeric_limits<float>::infinity()};
+        if (i < n) {
+            const T r2 = cen[4 * i + 3] * cen[4 * i + 3];   // as pack_scene: r.powi(2) in T
+            f[0] = (float)cen[4 * i]; f[1] = (float)cen[4 * i + 1]; f[2] = (float)cen[4 * i + 2];
+            const double c1 = std::fabs((double)f[0]) + std::fabs((double)f[1]) + std::fabs((double)f[2]);
+            const bool finite = std::isfinite(key[i]) && std::isfinite((double)r2) && std::isfinite(c1);
+            if (!finite || key[i] > kExactRatio * median) {
+                f[3] = std::numeric_limits<float>::infinity();
+            } else {
+                f[3] = up32((double)r2);
+                cm = std::max(cm, c1);
+                rm = std::max(rm, (double)f[3]);
+            }
+        }
+        const uint32_t g = i / 4, j = i % 4;
+        for (int q = 0; q < 4; ++q) grp[(size_t)16 * g + 8 * (j / 2) + 2 * q + (j % 2)] = f[q];   // pair-interleaved
+    }
+    cmax = up32(cm);
+    r2max = up32(rm);
+}
+
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     if (!c || !s) return fail(RT_ERR_INVALID, "rt_context_set_scene: NULL argument");
     if (s->n_spheres && (!s->center || !s->radius || !s->material || !s->materials))
@@ -1061,6 +1223,14 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     int rc;
     if ((rc = up(&c->sph64, g64.data(), g64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->sph32, g32.data(), g32.size() * sizeof(float))) != RT_OK) return rc;
+    {
+        std::vector<float> f64g, f32g;
+        uint32_t nf = 0;
+        pack_filter(c64, s->n_spheres, f64g, nf, c->f_cmax64, c->f_r2max64);
+        pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32);
+        if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
+    }
     HIPCHK(hipMalloc(&c->cam64, g64.size() * sizeof(double)));
     HIPCHK(hipMalloc(&c->cam32, g32.size() * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
@@ -1105,6 +1275,14 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.sph = (const T*)(f64 ? c->sph64 : c->sph32);
     p.cen = (const T*)(f64 ? c->cen64 : c->cen32);
     p.n_groups = f64 ? c->n_groups64 : c->n_groups32;
+    p.fsph = (const float*)(f64 ? c->fsph64 : c->fsph32);
+    p.n_fgroups = c->n_fgroups;
+    p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
+    p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
+    {   // diagnostics: every general-sweep group through the exact test
+        const char* e = getenv("RT_FILTER_OFF");
+        if (e && atoi(e) != 0) p.f_cmax = std::numeric_limits<float>::infinity();
+    }
     p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
     p.smat = c->smat;
     p.n_spheres = c->n_spheres;
@@ -1236,7 +1414,7 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     for (int i = 0; i < kSegShards; ++i)
         for (int j = 0; j < 4; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
     if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
-        fprintf(stderr, "rt_kstats: taken_groups %llu hit_branches %llu hit_lanes %llu camera_iters %llu\n",
+        fprintf(stderr, "rt_kstats: general taken_groups %llu sweeps %llu  camera taken_groups %llu sweeps %llu\n",
                 (unsigned long long)kst[0], (unsigned long long)kst[1], (unsigned long long)kst[2], (unsigned long long)kst[3]);
     for (int i = 0; i < kSegShards; ++i) {
         total += segs[(size_t)i * kSegStride];

@@ -420,3 +420,50 @@ def test_long_paths_replay(renderer, depth, prec):
     lin, st = assert_parity(renderer, flat, cam_for(16, 9), depth, 24, abi.RT_FLAG_ROOT2 | prec)
     # bounce_iters sums each pixel's K = min(depth, longest path + 1); measured: 4224 at depth 60
     assert st.bounce_iters > 9 * 16 * (20 if depth < 64 else 40)
+
+
+# ---- general-sweep distance filter (nearest_hit / filter_group): never changes a result ----
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32, abi.RT_FLAG_ROOT2 | abi.RT_FLAG_F32, abi.RT_FLAG_MODE_SCALAR])
+def test_filter_off_same_image(renderer, scene_100, flags, monkeypatch):
+    """RT_FILTER_OFF=1 sends every general-sweep group through the exact test (the path lanes with
+    a degenerate basis take); the image must equal both the filtered one and the oracle."""
+    cam = cam_for(64, 36)
+    lin_f, _ = assert_parity(renderer, scene_100, cam, 50, 16, flags)
+    monkeypatch.setenv("RT_FILTER_OFF", "1")
+    lin_x, _ = assert_parity(renderer, scene_100, cam, 50, 16, flags)
+    np.testing.assert_array_equal(lin_f, lin_x)
+
+
+def _transformed(flat, scale, offset):
+    return rt.FlatScene(flat.center * scale + offset, flat.radius * scale, flat.material, flat.materials)
+
+
+@pytest.mark.parametrize("scale,offset", [(1e3, 0.0), (1.0, 3e4), (1e-3, 0.0), (37.0, -2.5e3)])
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_filter_scene_scales(renderer, scene_100, scale, offset, flags):
+    """The filter margin scales with (max|c|_1 + |o|_1)^2: far-from-origin and tiny scenes keep
+    bit parity (the camera moves with the scene)."""
+    flat = _transformed(scene_100, scale, offset)
+    kw = dict(rt.MAIN_CAMERA)
+    kw["center"] = tuple(np.array(kw["center"]) * scale + offset)
+    kw["look_at"] = tuple(np.array(kw["look_at"]) * scale + offset)
+    kw["focal_length"] = kw["focal_length"] * scale
+    cam = rt.camera_new_py(48, 27, **kw)
+    assert_parity(renderer, flat, cam, 50, 8, flags)
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_filter_many_exact_spheres(renderer, flags):
+    """Radii spanning six decades: many spheres exceed 8x the median |c|_1 + r and get r2f = +inf
+    ("always exact"), the rest share a margin set by the largest of them."""
+    rng = np.random.default_rng(11)
+    n = 61
+    r = 10.0 ** rng.uniform(-2, 4, n)
+    dirs = rng.standard_normal((n, 3))
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    c = dirs * (r[:, None] + rng.uniform(2.0, 30.0, (n, 1)))
+    mats = [rt.Lambertian((0.6, 0.5, 0.4)), rt.Metal((0.8, 0.8, 0.9), 0.05), rt.Dielectric(1.5, False)]
+    flat = rt.FlatScene(c, r, rng.integers(0, 3, n).astype(np.uint32), mats)
+    cam = rt.camera_new_py(40, 30, 2.0, 60.0, (0.0, 0.0, 0.0), (1.0, 0.2, 0.3), (0.0, 1.0, 0.0), 0.0)
+    assert_parity(renderer, flat, cam, 50, 8, flags)
