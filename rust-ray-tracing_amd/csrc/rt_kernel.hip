@@ -98,6 +98,7 @@ template <typename T> struct KParams {
     uint32_t vbytes, sbytes;   // trace_paths: value-array bytes, per-slot record bytes (PScratch)
     const T* camsph;           // camera-origin table {oc, c} in the sph layout (pinhole launches)
     const float* fsph;         // filter stream: fp32 groups of 4 {cx, cy, cz, r2f} (layout above)
+    const float* camf;         // camera filter table: fp32 groups of 4 {ocx, ocy, ocz, sc} (build_cam_table)
     uint32_t n_fgroups;
     float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
 };
@@ -208,6 +209,29 @@ __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 
     return __builtin_amdgcn_bitop3_b32(t, __float_as_uint(r1.y), 0u, 0x3F);
 }
 
+// The camera-batch filter for one 4-sphere group (nearest_hit, CAMT under Q1): per sphere pair
+// hb' = ocx*dx^ + ocy*dy^ + ocz*dz^ and t = hb' + sc; returns t0 | t1 | t2 | t3, whose sign bit
+// is set iff some sphere passes (t < 0).  K0 = {dx^, dy^}, K1 = {dz^, -} broadcast with op_sel;
+// the two pairs are interleaved so no packed result is read by the next instruction.
+__device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur, f2 K0, f2 K1) {
+    const f2 ox0 = {cur.v[0], cur.v[1]}, oy0 = {cur.v[2], cur.v[3]}, oz0 = {cur.v[4], cur.v[5]}, sc0 = {cur.v[6], cur.v[7]};
+    const f2 ox1 = {cur.v[8], cur.v[9]}, oy1 = {cur.v[10], cur.v[11]}, oz1 = {cur.v[12], cur.v[13]}, sc1 = {cur.v[14], cur.v[15]};
+    f2 t0, t1;
+    asm volatile(
+        "v_pk_mul_f32 %[t0], %[ox0], %[K0] op_sel_hi:[1,0]\n\t"                         // ocx*dx^
+        "v_pk_mul_f32 %[t1], %[ox1], %[K0] op_sel_hi:[1,0]\n\t"
+        "v_pk_fma_f32 %[t0], %[oy0], %[K0], %[t0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"   // + ocy*dy^
+        "v_pk_fma_f32 %[t1], %[oy1], %[K0], %[t1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[t0], %[oz0], %[K1], %[t0] op_sel_hi:[1,0,1]\n\t"                  // + ocz*dz^
+        "v_pk_fma_f32 %[t1], %[oz1], %[K1], %[t1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_add_f32 %[t0], %[t0], %[sc0]\n\t"                                           // + sc
+        "v_pk_add_f32 %[t1], %[t1], %[sc1]"
+        : [t0] "=&v"(t0), [t1] "=&v"(t1)
+        : [ox0] "s"(ox0), [oy0] "s"(oy0), [oz0] "s"(oz0), [sc0] "s"(sc0), [ox1] "s"(ox1), [oy1] "s"(oy1),
+          [oz1] "s"(oz1), [sc1] "s"(sc1), [K0] "v"(K0), [K1] "v"(K1));
+    return (__float_as_uint(t0.x) | __float_as_uint(t0.y) | __float_as_uint(t1.x)) | __float_as_uint(t1.y);
+}
+
 // The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
 // index of the nearest valid hit (-1: the sky, :421-424) and its t.
 // SCALAR selects Sphere::hit + Scene::hit (objects.rs:216-247, ray_tracing.rs:231-235): no FMA,
@@ -259,7 +283,61 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     auto is_cand = [](uint32_t m) -> bool { return (int32_t)m < 0; };
     // Per-sphere test inside a taken group: a float superset of cand (hb == +0 passes too).
     auto cand_f = [&](T hb, T disc) -> bool { return kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)); };
-    if constexpr (CAMT) {
+    if constexpr (CAMT && !kBothRoots) {
+        // Camera batches under Q1 (hit_packed; root1 only).  A valid hit needs hb < 0 (root1 =
+        // (-hb - sd)/a > 0) and disc >= 0, i.e. -hb >= sqrt(a c): with d^ = d / |d| (fp32) and
+        // hb' = oc.d^, the filter passes a sphere iff hb' + sc < 0, where the camera filter table
+        // holds sc = sqrt(c) - 24 u |oc| - 1e-20 (build_cam_table; +inf for c <= 0: a camera inside
+        // or on the sphere never hits it under Q1).  The 24 u covers the reference's rounding of
+        // hb and disc, d^'s and hb''s rounding and the fp32 conversion of fp64 rays (a first-order
+        // bound is ~13 u; fuzzed worst case 3.7 u, tests/test_filter_margin.py).  4 packed ops per
+        // sphere pair against the exact 5 (fp32) or 10 fp64 ops; taken groups rerun the exact
+        // test from the camera-origin table.
+        const auto& qa = *cold_args<T>();
+        cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.camf, 64);
+        cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.camsph, 64);
+        const uint32_t ngf = qa.n_fgroups;
+        const float fdx = (float)d.x, fdy = (float)d.y, fdz = (float)d.z;
+        const float inv = 1.0f / sqrtf(__builtin_fmaf(fdz, fdz, __builtin_fmaf(fdy, fdy, fdx * fdx)));
+        const f2 K0 = {fdx * inv, fdy * inv}, K1 = {fdz * inv, 0.0f};
+        auto exact4 = [&](uint32_t g) {
+            KSTAT(2);
+            if constexpr (sizeof(T) == 4) {
+                const SphGroup<T> cur = load_group(fe, g);
+                const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+                const f2 na = {-a, -a};
+                f2 hb[2], disc[2];
+#pragma unroll
+                for (uint32_t q = 0; q < 2; ++q) {
+                    const T* v = &cur.v[8 * q];
+                    const f2 ocx = {v[0], v[1]}, ocy = {v[2], v[3]}, ocz = {v[4], v[5]}, c = {v[6], v[7]};
+                    hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));
+                    disc[q] = fma2(hb[q], hb[q], na * c);
+                }
+                const uint32_t i0 = 4 * g;
+                if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, i0);
+                if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, i0 + 1);
+                if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, i0 + 2);
+                if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, i0 + 3);
+            } else {
+                const SphGroup<T> c0 = load_group(fe, 2 * g), c1 = load_group(fe, 2 * g + 1);
+                T hb[4], disc[4];
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j) {
+                    const T* v = j < 2 ? &c0.v[4 * j] : &c1.v[4 * (j - 2)];
+                    hb[j] = pk_dot(mk(v[0], v[1], v[2]), d);
+                    disc[j] = fma(hb[j], hb[j], -a * v[3]);
+                }
+#pragma unroll
+                for (uint32_t j = 0; j < 4; ++j)
+                    if (cand_f(hb[j], disc[j])) hit(hb[j], disc[j], 4 * g + j);
+            }
+        };
+        auto group = [&](const SphGroup<float>& cur, uint32_t g) {
+            if (is_cand(cam_filter_group(cur, K0, K1))) exact4(g);
+        };
+        sphere_loop(ff, ngf, group);
+    } else if constexpr (CAMT) {
         // Camera batches: {ocx, ocy, ocz, c} from the camera-origin table, so the exact test is
         // hb (3 ops) and disc (2).  Filter on the exact sign bits: a sphere can only be hit if
         // disc >= +0 (disc is never -0: fma(hb, hb, -(a*c)) and hb*hb - a*c round an exact zero
@@ -335,7 +413,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // basis degenerates (d nearly parallel to y) or whose origin is huge get m = +inf and a
         // zero basis, so every group is taken for them (D = +inf, or a positive default NaN for a
         // -inf dummy, which only costs an exact test).  RT_FILTER_OFF=1 (host, diagnostics and
-        // tests) sets f_cmax = +inf: every lane degenerate, every group exact.
+        // tests) sets f_cmax = +inf (every lane degenerate, every group exact) and sc = -inf in
+        // the camera filter table.
         const auto& qa = *cold_args<T>();
         cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.fsph, 64);
         cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
@@ -522,22 +601,43 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
 // (objects.rs:252, 256; scalar: 217, 221) are the same for all of them.  Computed once per launch
 // with the same operations, in the sph group layout with {cx, cy, cz, r^2} -> {ocx, ocy, ocz, c};
 // a dummy (r^2 = -inf) gets c = +inf, so its discriminant is still -inf.
+// Also the camera filter table (fp32, groups of 4 spheres), used by the camera-batch sweep under Q1.
 template <typename T, bool SCALAR>
-__global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, T ox, T oy, T oz) {
+__global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* camf, uint32_t n_fslots, T ox, T oy,
+                                T oz, uint32_t pass_all) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_slots) return;
+    if (i >= n_slots && i >= n_fslots) return;
     constexpr uint32_t G = kGroup<T>, NE = 64 / sizeof(T);
     const uint32_t g = i / G, j = i % G;
     auto at = [&](uint32_t f) -> uint32_t {
         return sizeof(T) == 4 ? g * NE + 8 * (j / 2) + 2 * f + (j % 2) : g * NE + 4 * j + f;
     };
-    const T cx = sph[at(0)], cy = sph[at(1)], cz = sph[at(2)], r2 = sph[at(3)];
-    const T ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;
-    const T c = SCALAR ? ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2 : fma(ocz, ocz, fma(ocy, ocy, ocx * ocx)) - r2;
-    cam[at(0)] = ocx;
-    cam[at(1)] = ocy;
-    cam[at(2)] = ocz;
-    cam[at(3)] = c;
+    T ocx = T(0), ocy = T(0), ocz = T(0), c = T(INFINITY);   // slots past the exact table: dummies
+    if (i < n_slots) {
+        const T cx = sph[at(0)], cy = sph[at(1)], cz = sph[at(2)], r2 = sph[at(3)];
+        ocx = ox - cx; ocy = oy - cy; ocz = oz - cz;
+        c = SCALAR ? ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2 : fma(ocz, ocz, fma(ocy, ocy, ocx * ocx)) - r2;
+        cam[at(0)] = ocx;
+        cam[at(1)] = ocy;
+        cam[at(2)] = ocz;
+        cam[at(3)] = c;
+    }
+    if (i < n_fslots) {
+        // Camera filter record (fp32 layout, nearest_hit CAMT + Q1): {ocx, ocy, ocz} in fp32 and
+        // sc = sqrt(c) - 24 u |oc| - 1e-20 rounded down (u = 2^-24), or +inf when c <= 0 (the
+        // camera is inside or on the sphere: under Q1 root1 <= 0, never a hit) or NaN.
+        const double cd = (double)c;
+        const double ocn = sqrt((double)ocx * (double)ocx + (double)ocy * (double)ocy + (double)ocz * (double)ocz);
+        float sc = pass_all ? -INFINITY : INFINITY;   // pass_all: RT_FILTER_OFF (every group exact)
+        if (cd > 0.0 && !pass_all) {
+            const double v = sqrt(cd) - 0x1.8p-20 * ocn - 1e-20;   // 24 u = 1.5 * 2^-20
+            sc = (float)v;
+            if ((double)sc > v) sc = nextafterf(sc, -INFINITY);
+        }
+        const uint32_t fg = i / 4, fj = i % 4;
+        float* out = camf + 16 * fg + 8 * (fj / 2) + (fj % 2);
+        out[0] = (float)ocx; out[2] = (float)ocy; out[4] = (float)ocz; out[6] = sc;
+    }
 }
 
 // Make this wave's earlier global stores visible to its later loads (other lanes, same wave).
@@ -1010,6 +1110,7 @@ struct rt_context {
     uint32_t n_fgroups = 0;
     float f_cmax64 = 0, f_r2max64 = 0, f_cmax32 = 0, f_r2max32 = 0;
     void* cam64 = nullptr; void* cam32 = nullptr;   // camera-origin tables (same size; rebuilt per launch)
+    void* camf64 = nullptr; void* camf32 = nullptr; // camera filter tables (fp32 layout; rebuilt per launch)
     void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
@@ -1088,6 +1189,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->sph64); (void)hipFree(c->sph32); (void)hipFree(c->mat64); (void)hipFree(c->mat32);
     (void)hipFree(c->cam64); (void)hipFree(c->cam32);
     c->cam64 = c->cam32 = nullptr;
+    (void)hipFree(c->camf64); (void)hipFree(c->camf32);
+    c->camf64 = c->camf32 = nullptr;
     (void)hipFree(c->fsph64); (void)hipFree(c->fsph32);
     c->fsph64 = c->fsph32 = nullptr;
     (void)hipFree(c->cen64); (void)hipFree(c->cen32);
@@ -1230,6 +1333,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32);
         if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
+        HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
+        HIPCHK(hipMalloc(&c->camf32, f32g.size() * sizeof(float)));
     }
     HIPCHK(hipMalloc(&c->cam64, g64.size() * sizeof(double)));
     HIPCHK(hipMalloc(&c->cam32, g32.size() * sizeof(float)));
@@ -1279,9 +1384,11 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_fgroups = c->n_fgroups;
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
-    {   // diagnostics: every general-sweep group through the exact test
+    bool filter_off = false;
+    {   // diagnostics: every general-sweep and camera-sweep group through the exact test
         const char* e = getenv("RT_FILTER_OFF");
-        if (e && atoi(e) != 0) p.f_cmax = std::numeric_limits<float>::infinity();
+        filter_off = e && atoi(e) != 0;
+        if (filter_off) p.f_cmax = std::numeric_limits<float>::infinity();
     }
     p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
     p.smat = c->smat;
@@ -1323,10 +1430,12 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W) : pick_kernel<T, false>(flags, W);
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
-        const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>;
+        p.camf = (const float*)(f64 ? c->camf64 : c->camf32);
+        const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>, n_fslots = (p.n_fgroups + 1) * 4;
+        const uint32_t n_thr = n_slots > n_fslots ? n_slots : n_fslots;
         auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
-        hipLaunchKernelGGL(build, dim3((n_slots + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
-                           p.center[0], p.center[1], p.center[2]);
+        hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
+                           (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off);
         HIPCHK(hipGetLastError());
     }
     int per_cu = 0;

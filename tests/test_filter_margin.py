@@ -1,4 +1,4 @@
-"""The general-sweep distance filter never drops a sphere the reference could hit (CPU).
+"""The sweep filters never drop a sphere the reference could hit (CPU).
 
 rt_kernel.hip tests every bounced ray against every sphere with a cheap fp32 filter first
 (x^2 + y^2 <= r^2 + m in a basis perpendicular to the ray, nearest_hit / filter_group) and runs
@@ -44,3 +44,31 @@ def test_filter_is_conservative(fuzz_bin, mode):
     assert r.returncode == 0 and misses == 0, line
     assert accepted > 1000000, line          # the cases really sit on both sides of tangency
     assert worst < MARGIN_U / 4, line        # >= 4x headroom over the worst case found
+
+
+@pytest.fixture(scope="module")
+def cam_fuzz_bin(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("camfuzz") / "cam_filter_fuzz")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", out, os.path.join(HERE, "cam_filter_fuzz.c"), "-lm"],
+                   check=True)
+    return out
+
+
+def test_cam_margin_constant_matches_kernel():
+    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    assert "sqrt(cd) - 0x1.8p-20 * ocn - 1e-20" in src      # 24 u |oc| + 1e-20
+    assert "sqrt(c64) - 24 * u * ocn - 1e-20" in open(os.path.join(HERE, "cam_filter_fuzz.c")).read()
+
+
+@pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
+def test_camera_filter_is_conservative(cam_fuzz_bin, f64):
+    """Camera batches under Q1: every valid root1 passes hb' + sc < 0 (margin 24 u; >= 4x headroom)."""
+    r = subprocess.run([cam_fuzz_bin, "3000000", str(f64), str(0x5851F42D4C957F2D + f64)], capture_output=True,
+                       text=True, timeout=300)
+    fields = r.stdout.split()
+    misses = int(fields[fields.index("misses") + 1])
+    valid = int(fields[fields.index("valid") + 1])
+    worst = float(fields[-1])
+    assert r.returncode == 0 and misses == 0, r.stdout
+    assert valid > 1000000, r.stdout
+    assert worst < 24.0 / 4, r.stdout

@@ -467,3 +467,23 @@ def test_filter_many_exact_spheres(renderer, flags):
     flat = rt.FlatScene(c, r, rng.integers(0, 3, n).astype(np.uint32), mats)
     cam = rt.camera_new_py(40, 30, 2.0, 60.0, (0.0, 0.0, 0.0), (1.0, 0.2, 0.3), (0.0, 1.0, 0.0), 0.0)
     assert_parity(renderer, flat, cam, 50, 8, flags)
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32, abi.RT_FLAG_MODE_VECTORIZED])
+def test_camera_inside_and_on_spheres(renderer, flags):
+    """Camera-batch filter under Q1: spheres enclosing the camera (c < 0) and one whose surface
+    passes through the camera centre (c == 0 exactly) get sc = +inf -- under Q1 root1 <= 0 for
+    them, so the reference never hits them either; the spheres in view keep bit parity."""
+    cam_kw = dict(rt.MAIN_CAMERA)
+    o = np.array(cam_kw["center"])
+    rng = np.random.default_rng(5)
+    c = [o, o + np.array([2.0, 0.0, 0.0])]                       # enclosing r=60; on-surface r=2
+    r = [60.0, 2.0]
+    for _ in range(40):
+        p = rng.uniform(-4, 4, 3) * np.array([1, 0.3, 1])
+        c.append(p); r.append(rng.uniform(0.2, 0.8))
+    mats = [rt.Lambertian((0.7, 0.6, 0.5)), rt.Metal((0.9, 0.9, 0.9), 0.1), rt.Dielectric(1.5, False)]
+    mi = np.concatenate([[0, 1], rng.integers(0, 3, 40)]).astype(np.uint32)
+    flat = rt.FlatScene(np.array(c), np.array(r), mi, mats)
+    lin, st = assert_parity(renderer, flat, cam_for(48, 27), 50, 8, flags)
+    assert st.ray_segments > 48 * 27 * 8
