@@ -9,9 +9,15 @@ the RGB8 shards over RCCL and re-interleaves them (the north star's tiles + gath
 fixed as N grows -> "scaling": "strong").  Inputs (scene SoA, camera) are resident in HBM before
 the timed region.  Rank 0 prints one JSON line.
 
-roofline: the trace kernel is FP VALU-bound (no MFMA, ~0.09 B/sample of HBM traffic).
-  algorithmic FLOP per launch = 17 * n_spheres * ray_segments   (segments counted
-  in-kernel), achieved = that / average launch duration (HIP events on the launch stream).
+roofline: the trace kernel is VALU-issue-bound (no MFMA; HBM traffic ~5 % of bandwidth).
+  algorithmic FLOP per launch = 17 * n_spheres * ray_segments   (the reference's
+  mandatory 17-FLOP sphere test per segment and sphere; segments counted in-kernel), achieved = that /
+  average launch duration (HIP events on the launch stream), peak = the packed-FP32 VALU peak for
+  both dtypes: fp64 rays also sweep the spheres with the packed-FP32 filters, fp64
+  arithmetic is only used on filter candidates.  The filters spend fewer instructions per (ray,
+  sphere) than the 17-FLOP test, so this frac is an effective (brute-force-equivalent) rate; the
+  physical bound is VALU issue, reported as valu_issue_frac = VALU instructions per launch (PMC,
+  profiles/traffic.json) * 4 cycles / (1024 SIMDs * launch time * 2.4 GHz).
 cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>) on this host's
   cores over a bounded strided pixel sample of the same workload.
 """
@@ -26,7 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rust-ray-tracing_amd"))
 
 FP32_VALU_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (packed FP32 vector)
-FP64_VALU_PEAK_TF = 78.6    # MI355X FP64 vector (spec)
+N_SIMD, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs; peak engine clock (one wave64 VALU per 4 cycles)
 FLOP_PER_SPHERE_TEST = 17
 
 
@@ -183,13 +189,14 @@ def main():
         launch_s = (kernel_ms / 1e3) / args.steps
         flop_launch = FLOP_PER_SPHERE_TEST * n_sph * (segs / args.steps)
         achieved = flop_launch / launch_s / 1e12
-        peak = FP32_VALU_PEAK_TF if args.precision == "f32" else FP64_VALU_PEAK_TF
-        traffic = None
+        peak = FP32_VALU_PEAK_TF
+        traffic, valu_insts = None, None
         try:
             with open(args.traffic) as f:
                 tr = json.load(f)
             key = f"{args.config}:{args.precision}:{world}"
             traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
+            valu_insts = tr.get(key, {}).get("valu_insts_per_launch")
         except (OSError, ValueError):
             pass
         line = {
@@ -222,6 +229,8 @@ def main():
                 "traffic": traffic,
                 "flop_per_launch": flop_launch,
                 "launch_ms": round(launch_s * 1e3, 3),
+                "valu_issue_frac": (round(valu_insts * 4 / (N_SIMD * launch_s * CLOCK_HZ), 4)
+                                    if valu_insts else None),
             },
             "ray_segments_per_sample": round(segs_total / samples, 5),
             "lane_utilisation": round(st.ray_segments / max(1, st.lane_slots), 4),
