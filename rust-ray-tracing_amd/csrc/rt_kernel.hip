@@ -101,6 +101,7 @@ template <typename T> struct KParams {
     const float* camf;         // camera filter table: fp32 groups of 4 {ocx, ocy, ocz, sc} (build_cam_table)
     uint32_t n_fgroups;
     float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
+    float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
 };
 
 constexpr int kSegShards = 256;
@@ -173,13 +174,14 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
 }
 
 // The general-sweep filter for one 4-sphere group (nearest_hit): per sphere pair
-//   x = cx*e1x + (cz*e1z - oe1),  y = cx*e2x + (cy*e2y + (cz*e2z - oe2)),  D = (r2f + m - y^2) - x^2
+//   x = cx*e1x + (cz*e1z - oe1),  y = cx*e2x + (cy*e2y + (cz*e2z - oe2)),  D = (r2f - y^2) - x^2
 // in packed FP32 (two spheres per op), then acc = ~(D0 & D1 & D2 & D3) on the sign bits.  The
-// per-lane constants come two to a VGPR pair, K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, m},
-// K3 = {-oe1, -oe2}, and each use broadcasts one half with op_sel / op_sel_hi (the compiler
-// materialises such splats as extra VGPR pairs).  The two pairs are interleaved so that no packed
-// result is read by the next instruction (the one-wait-state packed-FP32 read hazard the compiler
-// pads with s_nop).  16 packed ops, then v_and3 + v_bitop3 on the sign bits.
+// per-lane constants (the basis already scaled by the margin, nearest_hit) come two to a VGPR
+// pair, K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, -}, K3 = {-oe1, -oe2}, and each use
+// broadcasts one half with op_sel / op_sel_hi (the compiler materialises such splats as extra VGPR
+// pairs).  The two pairs are interleaved so that no packed result is read by the next instruction
+// (the one-wait-state packed-FP32 read hazard the compiler pads with s_nop).  14 packed ops, then
+// v_and3 + v_bitop3 on the sign bits.
 __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3) {
     const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
     const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
@@ -193,12 +195,10 @@ __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 
         "v_pk_fma_f32 %[b0], %[cy0], %[K1], %[b0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"   // cy*e2y + .
         "v_pk_fma_f32 %[a1], %[cx1], %[K0], %[a1] op_sel_hi:[1,0,1]\n\t"
         "v_pk_fma_f32 %[b1], %[cy1], %[K1], %[b1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_add_f32 %[r0], %[rr0], %[K2] op_sel:[0,1] op_sel_hi:[1,1]\n\t"              // r2f + m
         "v_pk_fma_f32 %[b0], %[cx0], %[K1], %[b0] op_sel_hi:[1,0,1]\n\t"                  // y = cx*e2x + .
-        "v_pk_add_f32 %[r1], %[rr1], %[K2] op_sel:[0,1] op_sel_hi:[1,1]\n\t"
         "v_pk_fma_f32 %[b1], %[cx1], %[K1], %[b1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[r0], %[b0], %[b0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"       // - y^2
-        "v_pk_fma_f32 %[r1], %[b1], %[b1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[r0], %[b0], %[b0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"      // r2f - y^2
+        "v_pk_fma_f32 %[r1], %[b1], %[b1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
         "v_pk_fma_f32 %[r0], %[a0], %[a0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"       // D = . - x^2
         "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
         : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
@@ -399,22 +399,23 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         //
         // Filter: with e1, e2 an orthonormal basis of the plane perpendicular to d (e1 has no y
         // component), x = (c - o).e1 and y = (c - o).e2 are the centre's offset from the ray's
-        // line, so the line meets the sphere iff x^2 + y^2 <= r^2.  Per sphere pair that is
-        // x: 2 packed FMAs, y: 3, r2f + m: 1, D = r2f + m - x^2 - y^2: 2 -- 8 ops against the
-        // exact test's 12.  The margin m = 48 u ((max|c|_1 + |o|_1)^2 + max r2f), u = 2^-24,
-        // covers the reference's own rounding of disc (a sphere it computes disc >= 0 for may lie
-        // slightly outside), the filter's basis and rounding errors, and for fp64 rays the
-        // conversion to fp32: a first-order bound is ~30 u, 80M adversarial
-        // near-tangent cases need at most 5 u (tests/test_filter_margin.py).  So every sphere the
-        // reference could hit passes; a group with any passing sphere recomputes all four exactly
-        // from the exact stream, and only the exact values ever reach hit().
+        // line, so the line meets the sphere iff x^2 + y^2 <= r^2.  The margin
+        // m = 48 u ((max|c|_1 + |o|_1)^2 + max r2f), u = 2^-24, covers the reference's own rounding
+        // of disc (a sphere it computes disc >= 0 for may lie slightly outside), the filter's basis
+        // and rounding errors, and for fp64 rays the conversion to fp32: a first-order bound is
+        // ~30 u, 80M adversarial near-tangent cases need at most 5 u
+        // (tests/test_filter_margin.py).  It is applied by scaling the basis by
+        // 1/sqrt(1 + m/r2min) (r2min: the smallest filtered r2f): the test x'^2 + y'^2 <= r2f is then
+        // x^2 + y^2 <= r2f (1 + m/r2min) >= r2f + m.  Per sphere pair: x 2 packed FMAs, y 3,
+        // D = r2f - y^2 - x^2 2 -- 7 ops against the exact test's 12.  So every sphere the reference
+        // could hit passes; a group with any passing sphere recomputes all four exactly from the
+        // exact stream, and only the exact values ever reach hit().
         // Spheres far outside the scene (|c|_1 + r > 8x the median, e.g. a ground sphere) would
         // inflate the margin for all: the host gives them r2f = +inf, "always exact".  Lanes whose
-        // basis degenerates (d nearly parallel to y) or whose origin is huge get m = +inf and a
-        // zero basis, so every group is taken for them (D = +inf, or a positive default NaN for a
-        // -inf dummy, which only costs an exact test).  RT_FILTER_OFF=1 (host, diagnostics and
-        // tests) sets f_cmax = +inf (every lane degenerate, every group exact) and sc = -inf in
-        // the camera filter table.
+        // basis degenerates (d nearly parallel to y) or whose origin is huge get a zero basis, so
+        // every real sphere passes for them (D = r2f; a -inf dummy never does).  RT_FILTER_OFF=1
+        // (host, diagnostics and tests) sets f_cmax = +inf (every lane degenerate, every group
+        // exact) and sc = -inf in the camera filter table.
         const auto& qa = *cold_args<T>();
         cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.fsph, 64);
         cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
@@ -423,24 +424,26 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         const float fox = (float)o.x, foy = (float)o.y, foz = (float)o.z;
         const float L = __builtin_fmaf(fdz, fdz, fdx * fdx);
         const float af = __builtin_fmaf(fdz, fdz, __builtin_fmaf(fdy, fdy, fdx * fdx));
-        const float s1 = 1.0f / sqrtf(L), s2 = 1.0f / sqrtf(L * af);
+        const float on = fabsf(fox) + fabsf(foy) + fabsf(foz);
+        const float pm = qa.f_cmax + on;
+        const float m = kFilterMargin * __builtin_fmaf(pm, pm, qa.f_r2max);
+        // Basis scaled by sg = 1/sqrt(1 + m/r2min): x'^2 + y'^2 <= r2f is x^2 + y^2 <= r2f (1 + m/r2min)
+        // >= r2f + m for every sphere (r2f >= r2min), so the margin needs no per-pair add.
+        const float sg = 1.0f / sqrtf(1.0f + m / qa.f_r2min);
+        const float s1 = (1.0f / sqrtf(L)) * sg, s2 = (1.0f / sqrtf(L * af)) * sg;
         float e1x = fdz * s1, e1z = -fdx * s1;
         float e2x = -(fdx * fdy) * s2, e2y = L * s2, e2z = -(fdy * fdz) * s2;
         float oe1 = __builtin_fmaf(foz, e1z, fox * e1x);
         float oe2 = __builtin_fmaf(foz, e2z, __builtin_fmaf(foy, e2y, fox * e2x));
-        const float on = fabsf(fox) + fabsf(foy) + fabsf(foz);
-        const float pm = qa.f_cmax + on;
-        float m = kFilterMargin * __builtin_fmaf(pm, pm, qa.f_r2max);
         // Degenerate lanes: L*af must not underflow (L >= 1e-15: d within ~3e-8 of the y axis), and
         // x^2, y^2 must stay finite (|c|_1 + |o|_1 <= 1e15), so D is never inf - inf.
-        if (!(L >= 1e-15f) || !(pm <= 1e15f)) {
+        if (!(L >= 1e-15f) || !(pm <= 1e15f)) {   // zero basis: x = y = 0, every real sphere passes
             e1x = e1z = e2x = e2y = e2z = 0.0f;
             oe1 = oe2 = 0.0f;
-            m = INFINITY;
         }
         // Two per-lane constants per VGPR pair; every use broadcasts one half through the packed
         // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
-        const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, m}, K3 = {-oe1, -oe2};
+        const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, 0.0f}, K3 = {-oe1, -oe2};
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222).
         auto exact4 = [&](uint32_t g) {
             KSTAT(0);
@@ -1108,7 +1111,7 @@ struct rt_context {
     void* sph64 = nullptr; void* sph32 = nullptr;   // grouped sphere records
     void* fsph64 = nullptr; void* fsph32 = nullptr; // fp32 filter streams (for fp64 / fp32 rays)
     uint32_t n_fgroups = 0;
-    float f_cmax64 = 0, f_r2max64 = 0, f_cmax32 = 0, f_r2max32 = 0;
+    float f_cmax64 = 0, f_r2max64 = 0, f_cmax32 = 0, f_r2max32 = 0, f_r2min64 = 0, f_r2min32 = 0;
     void* cam64 = nullptr; void* cam32 = nullptr;   // camera-origin tables (same size; rebuilt per launch)
     void* camf64 = nullptr; void* camf32 = nullptr; // camera filter tables (fp32 layout; rebuilt per launch)
     void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
@@ -1258,7 +1261,7 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
 // other spheres: max |c|_1 (rounded up) and max r2f.
 template <typename T>
 static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float>& grp, uint32_t& n_fgroups,
-                        float& cmax, float& r2max) {
+                        float& cmax, float& r2max, float& r2min) {
     n_fgroups = (n + 3) / 4;
     std::vector<double> key(n);
     for (uint32_t i = 0; i < n; ++i)
@@ -1275,7 +1278,22 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
         return f;
     };
+    // The kernel scales each lane's filter basis by 1/sqrt(1 + m/r2min), which inflates every r2f
+    // by the factor (1 + m/r2min) >= 1 + m/r2f.  A floor on r2f (tiny spheres filtered as if of the
+    // floor radius, conservative) keeps one tiny sphere from inflating all the others.
     double cm = 0.0, rm = 0.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const double c1 = std::fabs((double)(float)cen[4 * i]) + std::fabs((double)(float)cen[4 * i + 1]) +
+                          std::fabs((double)(float)cen[4 * i + 2]);
+        const double r2 = (double)(cen[4 * i + 3] * cen[4 * i + 3]);
+        if (std::isfinite(key[i]) && std::isfinite(r2) && std::isfinite(c1) && !(key[i] > kExactRatio * median)) {
+            cm = std::max(cm, c1);
+            rm = std::max(rm, r2);
+        }
+    }
+    const double floor2 = std::max(rm * 0x1.0p-10, cm * cm * 0x1.0p-16);
+    double rmin = std::numeric_limits<double>::infinity();
+    cm = 0.0; rm = 0.0;
     grp.assign((size_t)16 * (n_fgroups + 1), 0.0f);
     for (uint32_t i = 0; i < 4 * (n_fgroups + 1); ++i) {
         float f[4] = {0.0f, 0.0f, 0.0f, -std::numeric_limits<float>::infinity()};
@@ -1287,9 +1305,10 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
             if (!finite || key[i] > kExactRatio * median) {
                 f[3] = std::numeric_limits<float>::infinity();
             } else {
-                f[3] = up32((double)r2);
+                f[3] = up32(std::max((double)r2, floor2));
                 cm = std::max(cm, c1);
                 rm = std::max(rm, (double)f[3]);
+                rmin = std::min(rmin, (double)f[3]);
             }
         }
         const uint32_t g = i / 4, j = i % 4;
@@ -1297,6 +1316,7 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
     }
     cmax = up32(cm);
     r2max = up32(rm);
+    r2min = std::isfinite(rmin) ? (float)rmin : 0.0f;   // exact: rmin is an fp32 value
 }
 
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
@@ -1329,8 +1349,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     {
         std::vector<float> f64g, f32g;
         uint32_t nf = 0;
-        pack_filter(c64, s->n_spheres, f64g, nf, c->f_cmax64, c->f_r2max64);
-        pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32);
+        pack_filter(c64, s->n_spheres, f64g, nf, c->f_cmax64, c->f_r2max64, c->f_r2min64);
+        pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32, c->f_r2min32);
         if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
         HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
@@ -1384,6 +1404,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_fgroups = c->n_fgroups;
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
+    p.f_r2min = f64 ? c->f_r2min64 : c->f_r2min32;
     bool filter_off = false;
     {   // diagnostics: every general-sweep and camera-sweep group through the exact test
         const char* e = getenv("RT_FILTER_OFF");

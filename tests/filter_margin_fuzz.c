@@ -1,8 +1,9 @@
 // Fuzz of the general-sweep distance filter (rt_kernel.hip: nearest_hit / filter_group), test
 // infrastructure for tests/test_filter_margin.py.  Claim checked: whenever the reference's own
 // discriminant is >= 0 for a (ray, sphere) -- so the reference may hit it -- the filter's
-// D = r2f + m - x^2 - y^2 computed exactly as the kernel does has its sign bit clear, i.e. the
-// filter passes the sphere and the exact test decides.  Cases are adversarial: the centre is put
+// D = r2f - y'^2 - x'^2, computed exactly as the kernel does (basis scaled by 1/sqrt(1 + m/r2min),
+// margin m = 48 u ((max|c|_1 + |o|_1)^2 + max r2f)), has its sign bit clear, i.e. the filter
+// passes the sphere and the exact test decides.  Cases are adversarial: the centre is put
 // at distance r(1 +- 5e-4 * 10^-6U) from the ray's line (near tangency), scene scales 0.1..1000,
 // radii 1e-3..1 of the scale, near-vertical and non-unit directions.
 // The reference formulas are objects.rs:252-257 (hit_packed, FMA where it writes mul_add) and
@@ -86,23 +87,29 @@ int main(int argc, char** argv) {
         float L = fmaf(fdz, fdz, fdx * fdx);
         float af = fmaf(fdz, fdz, fmaf(fdy, fdy, fdx * fdx));
         float s1 = 1.0f / sqrtf(L), s2 = 1.0f / sqrtf(L * af);
-        float e1x = fdz * s1, e1z = -fdx * s1;
-        float e2x = -(fdx * fdy) * s2, e2y = L * s2, e2z = -(fdy * fdz) * s2;
-        float oe1 = fmaf(foz, e1z, fox * e1x), oe2 = fmaf(foz, e2z, fmaf(foy, e2y, fox * e2x));
         float on = fabsf(fox) + fabsf(foy) + fabsf(foz);
-        // the kernel's m uses the scene-wide max |c|_1 and max r2f; this sphere's own values are
-        // lower bounds of those, so the margin tested here is never larger than the kernel's
+        // the kernel's m uses the scene-wide max |c|_1 and max r2f, and its r2min is the scene's
+        // smallest r2f; this sphere's own values bound those from the unfavourable side, so the
+        // inflation tested here (r2f * (1 + m / r2f) = r2f + m) is never larger than the kernel's
         float cmax = fabsf(cx) + fabsf(cy) + fabsf(cz);
         float pm = cmax + on;
         float m = KM * fmaf(pm, pm, r2f);
+        float r2min = r2f;
+        // basis scaled by sigma = 1/sqrt(1 + m/r2min): the test x'^2 + y'^2 <= r2f is
+        // x^2 + y^2 <= r2f (1 + m/r2min) >= r2f + m, with no per-pair add
+        float sg = 1.0f / sqrtf(1.0f + m / r2min);
+        float t1 = s1 * sg, t2 = s2 * sg;
+        float e1x = fdz * t1, e1z = -fdx * t1;
+        float e2x = -(fdx * fdy) * t2, e2y = L * t2, e2z = -(fdy * fdz) * t2;
+        float oe1 = fmaf(foz, e1z, fox * e1x), oe2 = fmaf(foz, e2z, fmaf(foy, e2y, fox * e2x));
         float x = fmaf(cx, e1x, fmaf(cz, e1z, -oe1));
         float y = fmaf(cx, e2x, fmaf(cy, e2y, fmaf(cz, e2z, -oe2)));
-        float Dv = fmaf(-x, x, fmaf(-y, y, r2f + m));
+        float Dv = fmaf(-x, x, fmaf(-y, y, r2f));
         uint32_t bits; memcpy(&bits, &Dv, 4);
         if (ref_ok) {
             ++acc;
             if (bits >> 31) ++miss;
-            double need = ((double)x * x + (double)y * y - r2f) / ((double)pm * pm + r2f) / 0x1.0p-24;
+            double need = (((double)x * x + (double)y * y) / ((double)sg * sg) - r2f) / ((double)pm * pm + r2f) / 0x1.0p-24;
             if (need > worst) worst = need;
         }
     }
