@@ -102,12 +102,14 @@ template <typename T> struct KParams {
     uint32_t n_fgroups;
     float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
     float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
+    const float* cull;         // camera cone-cull table: {wx, wy, wz, rp} per sphere (build_cam_table)
+    const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
 };
 
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
-constexpr int kWavesF64 = 5;
+constexpr int kWavesF64 = 4;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
@@ -239,6 +241,32 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
 // PackedHitRecords::update (objects.rs:249-290, 140-155).
 // CAMT: the ray starts at the camera centre and the sweep reads the camera-origin table
 // (build_cam_table): oc and c come precomputed, bit-identical to the per-ray values.
+// Sphere::hit_packed's root and PackedHitRecords::update (objects.rs:263-290, 140-155) for a
+// candidate whose discriminant is non-negative; SCALAR: Sphere::hit + Scene::hit's min_by_key
+// (objects.rs:227-234, ray_tracing.rs:231-235: the first minimum wins).
+template <typename T, bool root2, bool SCALAR>
+__device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_a, T& best_t, int& best) {
+    if constexpr (SCALAR) {
+        const T sd = sqrt(disc);
+        T root = (-hb - sd) / a;
+        if (!(root >= T(0.001) && root < T(INFINITY))) {
+            root = (-hb + sd) / a;
+            if (!(root >= T(0.001) && root < T(INFINITY))) return;
+        }
+        if (root < best_t) { best_t = root; best = (int)i; }
+        return;
+    }
+    const T sd = sqrt(disc);
+    const T r1 = (-hb - sd) * inv_a;                       // :270
+    bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
+    T root = r1;
+    if (root2 && !valid) {                                 // Q1 off: scalar semantics
+        root = (-hb + sd) * inv_a;                         // :271
+        valid = root >= T(0.001) && root < T(INFINITY);
+    }
+    if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
+}
+
 template <typename T, bool root2, bool SCALAR = false, bool CAMT = false>
 __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, const V3<T>& d, T& t_out) {
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
@@ -249,27 +277,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     // for a candidate whose discriminant is non-negative.  Exact pre-filter: with hb >= 0,
     // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
     KSTAT(CAMT ? 3 : 1);   // sweeps (one per wave)
-    auto hit = [&](T hb, T disc, uint32_t i) {
-        if constexpr (SCALAR) {   // objects.rs:227-234 and min_by_key (first minimum)
-            const T sd = sqrt(disc);
-            T root = (-hb - sd) / a;
-            if (!(root >= T(0.001) && root < T(INFINITY))) {
-                root = (-hb + sd) / a;
-                if (!(root >= T(0.001) && root < T(INFINITY))) return;
-            }
-            if (root < best_t) { best_t = root; best = (int)i; }
-            return;
-        }
-        const T sd = sqrt(disc);
-        const T r1 = (-hb - sd) * inv_a;                       // :270
-        bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
-        T root = r1;
-        if (root2 && !valid) {                                 // Q1 off: scalar semantics
-            root = (-hb + sd) * inv_a;                         // :271
-            valid = root >= T(0.001) && root < T(INFINITY);
-        }
-        if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
-    };
+    auto hit = [&](T hb, T disc, uint32_t i) { hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best); };
     // Spheres stream through the scalar cache in 64-byte groups; group g+1 is requested before
     // group g is tested so the K$ latency hides behind the group's VALU work.
     // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
@@ -505,6 +513,95 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
     return best;
 }
 
+// Camera-batch sweep with a wave-level cone cull (pinhole cameras; called by the whole wave, lanes
+// `v` carry a primary ray d from the camera centre).  The batch's rays all start at the centre O, so
+// they lie in the cone with apex O, axis a (the first ray's direction) and half-angle theta, where
+// sin(theta) = max over the batch of |d^ x a| (fp32, inflated by 8 u + 4 u relative).  A sphere can
+// only be hit by a ray of the batch if it meets that cone: with w = c - O, t = w.a and p = |w x a|,
+// the signed distance from the centre to the cone's generator line in the plane of a and w is
+// p cos(theta) - t sin(theta) (<= the distance to the cone), so the cull passes the sphere unless it
+// exceeds rp.  rp (build_cam_table) = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w|: the first term
+// covers the reference's own rounding of the discriminant (a sphere whose computed disc >= 0 lies
+// at most sqrt(r^2 + ~10 u |w|^2) from the ray's line, the same bound as the per-lane filters'), the
+// second the fp32 rounding of w, t, p, a and theta (~10 u |w|).  Lanes as spheres: one coalesced
+// 16-byte load and ~16 VALU per 64 spheres, then the exact test (objects.rs:252-257 on the
+// camera-origin table, bit-identical to the per-ray values) for the passing spheres only, in scene
+// order, so ties and the nearest hit are the reference's.  A batch whose rays spread over more than
+// ~30 degrees (tiny images) skips the cull and tests every sphere exactly.
+__device__ __forceinline__ float ufl(float x) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(x))); }
+
+template <typename T, bool root2, bool SCALAR>
+__device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const unsigned long long vm = __ballot(v);
+    const float fdx = v ? (float)d.x : 0.0f, fdy = v ? (float)d.y : 0.0f, fdz = v ? (float)d.z : 0.0f;
+    const int l0 = (int)__builtin_ctzll(vm);
+    float ax = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdx), l0));
+    float ay = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdy), l0));
+    float az = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdz), l0));
+    const float ia = 1.0f / sqrtf(__builtin_fmaf(az, az, __builtin_fmaf(ay, ay, ax * ax)));
+    // wave-uniform: keep the axis and the cone's (cos, sin) in SGPRs
+    ax = ufl(ax * ia);
+    ay = ufl(ay * ia);
+    az = ufl(az * ia);
+    // sin^2 of each ray's angle to the axis: |d^ x a|^2 / |d^|^2 (0 for idle lanes)
+    const float cx = __builtin_fmaf(fdy, az, -(fdz * ay)), cy = __builtin_fmaf(fdz, ax, -(fdx * az)),
+                cz = __builtin_fmaf(fdx, ay, -(fdy * ax));
+    const float dn2 = __builtin_fmaf(fdz, fdz, __builtin_fmaf(fdy, fdy, fdx * fdx));
+    const float s2 = v ? __builtin_fmaf(cz, cz, __builtin_fmaf(cy, cy, cx * cx)) / dn2 : 0.0f;
+    const float dt = __builtin_fmaf(fdz, az, __builtin_fmaf(fdy, ay, fdx * ax));
+    bool all = __ballot(v && !(dt > 0.5f)) != 0ull;   // some ray > 60 deg off the axis (or NaN)
+    uint32_t sm = __float_as_uint(s2);   // non-negative floats (and NaN above +inf) order as integers
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) sm = max(sm, (uint32_t)__shfl_xor((int)sm, o));
+    sm = __builtin_amdgcn_readfirstlane(sm);
+    const float S = ufl(__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f));
+    if (!(S < 0.5f)) all = true;
+    const float Cc = ufl(sqrtf(__builtin_fmaf(-S, S, 1.0f)));
+    const auto& q = *cold_args<T>();
+    const float4* cull = (const float4*)__builtin_assume_aligned(q.cull, 16);
+    cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
+    const uint32_t n = q.n_spheres;
+    const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
+    const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
+    T best_t = T(INFINITY);
+    int best = -1;
+    constexpr bool kBothRoots = root2 || SCALAR;
+    KSTAT(3);
+    float4 w = cull[lane];   // the table is padded with a whole dummy block: the prefetch stays in bounds
+    for (uint32_t base = 0; base < n; base += 64u) {
+        const float4 wc = w;
+        w = cull[base + 64u + lane];
+        const float t = __builtin_fmaf(wc.z, az, __builtin_fmaf(wc.y, ay, wc.x * ax));
+        const float px = __builtin_fmaf(wc.y, az, -(wc.z * ay)), py = __builtin_fmaf(wc.z, ax, -(wc.x * az)),
+                    pz = __builtin_fmaf(wc.x, ay, -(wc.y * ax));
+        const float pp = sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
+        const float f = __builtin_fmaf(pp, Cc, -(t * S));
+        const bool pass = all ? base + lane < n : !(f > wc.w);   // NaN passes
+        unsigned long long m = __ballot(pass);
+        while (m != 0ull) {
+            const uint32_t i = base + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            KSTAT(2);
+            const T ocx = cxt[4 * i], ocy = cxt[4 * i + 1], ocz = cxt[4 * i + 2], c = cxt[4 * i + 3];
+            if (v) {
+                T hb, disc;
+                if constexpr (SCALAR) {   // objects.rs:217-222
+                    hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
+                    disc = hb * hb - a * c;
+                } else {                  // objects.rs:255, 257
+                    hb = fma(ocz, d.z, fma(ocy, d.y, ocx * d.x));
+                    disc = fma(hb, hb, (-a) * c);
+                }
+                if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
+                    hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
+            }
+        }
+    }
+    t_out = best_t;
+    return best;
+}
+
 // The per-lane "next ray" stage.  Fresh lanes run Camera::get_ray (ray_tracing.rs:77-89; jitter
 // stream 0, disk stream 1); lanes that hit at bounce k run PackedHitRecords::finalize
 // (objects.rs:157-162) and Material::get_hit_result (materials.rs:54-147; stream 2).  Both draw one
@@ -607,9 +704,9 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
 // Also the camera filter table (fp32, groups of 4 spheres), used by the camera-batch sweep under Q1.
 template <typename T, bool SCALAR>
 __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* camf, uint32_t n_fslots, T ox, T oy,
-                                T oz, uint32_t pass_all) {
+                                T oz, uint32_t pass_all, T* camx, float* cull, uint32_t n_cull, uint32_t n_real) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_slots && i >= n_fslots) return;
+    if (i >= n_slots && i >= n_fslots && i >= n_cull) return;
     constexpr uint32_t G = kGroup<T>, NE = 64 / sizeof(T);
     const uint32_t g = i / G, j = i % G;
     auto at = [&](uint32_t f) -> uint32_t {
@@ -640,6 +737,26 @@ __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* c
         const uint32_t fg = i / 4, fj = i % 4;
         float* out = camf + 16 * fg + 8 * (fj / 2) + (fj % 2);
         out[0] = (float)ocx; out[2] = (float)ocy; out[4] = (float)ocz; out[6] = sc;
+    }
+    if (i < n_cull) {
+        // Per-sphere AoS copy of the camera-origin record, and the cone-cull record (camera_sweep):
+        // w = c - O in fp32 and rp = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w| rounded up (u = 2^-24);
+        // +inf (always tested) for non-finite values and under RT_FILTER_OFF, -inf for the padding.
+        T ex = T(0), ey = T(0), ez = T(0), ec = T(INFINITY);
+        float rp = -INFINITY;
+        if (i < n_real) {
+            ex = ocx; ey = ocy; ez = ocz; ec = c;
+            const double wx = (double)ocx, wy = (double)ocy, wz = (double)ocz;
+            const double wn2 = wx * wx + wy * wy + wz * wz, r2 = (double)sph[at(3)];
+            const double v = sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30;
+            rp = INFINITY;
+            if (!pass_all && v < 1e30) {
+                rp = (float)v;
+                if ((double)rp < v) rp = nextafterf(rp, INFINITY);
+            }
+        }
+        camx[4 * i] = ex; camx[4 * i + 1] = ey; camx[4 * i + 2] = ez; camx[4 * i + 3] = ec;
+        cull[4 * i] = -(float)ex; cull[4 * i + 1] = -(float)ey; cull[4 * i + 2] = -(float)ez; cull[4 * i + 3] = rp;
     }
 }
 
@@ -986,7 +1103,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         }
         T bt = T(0);
         int bi = -1;
+#ifndef RT_EXP_NO_CAMCULL
+        bi = camera_sweep<T, ROOT2, SC>(v, bd, bt);   // whole wave: lanes are spheres in the cull
+#else
         if (v) bi = nearest_hit<T, ROOT2, SC, true>(p, bd, bd, bt);
+#endif
         if (lane == 0) { wcount[wave][0] += (uint32_t)__popcll(vm); wcount[wave][1] += 64u; }
         const uint32_t depth = cold_args<T>()->depth;
         const bool skyhit = v && bi < 0;
@@ -1115,6 +1236,9 @@ struct rt_context {
     void* cam64 = nullptr; void* cam32 = nullptr;   // camera-origin tables (same size; rebuilt per launch)
     void* camf64 = nullptr; void* camf32 = nullptr; // camera filter tables (fp32 layout; rebuilt per launch)
     void* cen64 = nullptr; void* cen32 = nullptr;   // AoS centre tables
+    void* camx64 = nullptr; void* camx32 = nullptr; // per-sphere camera-origin records (rebuilt per launch)
+    void* cull64 = nullptr; void* cull32 = nullptr; // camera cone-cull records (fp32; rebuilt per launch)
+    uint32_t n_cull = 0;                            // records: n_spheres rounded up to 64, + 64 padding
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
     uint32_t* smat = nullptr;
@@ -1197,6 +1321,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->fsph64); (void)hipFree(c->fsph32);
     c->fsph64 = c->fsph32 = nullptr;
     (void)hipFree(c->cen64); (void)hipFree(c->cen32);
+    (void)hipFree(c->camx64); (void)hipFree(c->camx32); (void)hipFree(c->cull64); (void)hipFree(c->cull32);
+    c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
@@ -1358,6 +1484,11 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     }
     HIPCHK(hipMalloc(&c->cam64, g64.size() * sizeof(double)));
     HIPCHK(hipMalloc(&c->cam32, g32.size() * sizeof(float)));
+    c->n_cull = (s->n_spheres + 63u) / 64u * 64u + 64u;
+    HIPCHK(hipMalloc(&c->camx64, (size_t)4 * c->n_cull * sizeof(double)));
+    HIPCHK(hipMalloc(&c->camx32, (size_t)4 * c->n_cull * sizeof(float)));
+    HIPCHK(hipMalloc(&c->cull64, (size_t)4 * c->n_cull * sizeof(float)));
+    HIPCHK(hipMalloc(&c->cull32, (size_t)4 * c->n_cull * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->cen32, c32.data(), c32.size() * sizeof(float))) != RT_OK) return rc;
     if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
@@ -1452,11 +1583,14 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
         p.camf = (const float*)(f64 ? c->camf64 : c->camf32);
+        p.camx = (const T*)(f64 ? c->camx64 : c->camx32);
+        p.cull = (const float*)(f64 ? c->cull64 : c->cull32);
         const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>, n_fslots = (p.n_fgroups + 1) * 4;
-        const uint32_t n_thr = n_slots > n_fslots ? n_slots : n_fslots;
+        const uint32_t n_thr = std::max(std::max(n_slots, n_fslots), c->n_cull);
         auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
         hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
-                           (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off);
+                           (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off,
+                           (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres);
         HIPCHK(hipGetLastError());
     }
     int per_cu = 0;

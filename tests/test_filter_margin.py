@@ -72,3 +72,35 @@ def test_camera_filter_is_conservative(cam_fuzz_bin, f64):
     assert r.returncode == 0 and misses == 0, r.stdout
     assert valid > 1000000, r.stdout
     assert worst < 24.0 / 4, r.stdout
+
+
+@pytest.fixture(scope="module")
+def cone_fuzz_bin(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("conefuzz") / "cone_cull_fuzz")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", out, os.path.join(HERE, "cone_cull_fuzz.c"), "-lm"],
+                   check=True)
+    return out
+
+
+def test_cone_margin_constant_matches_kernel():
+    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    expr = "sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30"   # 64 u, 32 u
+    assert expr in src
+    assert expr.replace("r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
+    assert "__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f)" in src
+
+
+@pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
+def test_camera_cone_cull_is_conservative(cone_fuzz_bin, f64):
+    """Camera batches: a sphere any ray of the batch hits (Q1, root2 or scalar test) passes the
+    wave's cone cull; margin 64 u |w|^2 in r^2 with >= 4x headroom over the worst case found."""
+    r = subprocess.run([cone_fuzz_bin, "2000000", str(f64), str(0x2545F4914F6CDD1D + f64)], capture_output=True,
+                       text=True, timeout=300)
+    fields = r.stdout.split()
+    misses = int(fields[fields.index("misses") + 1])
+    hits = int(fields[fields.index("hits") + 1])
+    culled = int(fields[fields.index("culled") + 1])
+    worst = float(fields[-1])
+    assert r.returncode == 0 and misses == 0, r.stdout
+    assert hits > 1000000 and culled > 50000, r.stdout   # both sides of tangency are exercised
+    assert worst < 64.0 / 4, r.stdout

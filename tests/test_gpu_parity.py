@@ -487,3 +487,38 @@ def test_camera_inside_and_on_spheres(renderer, flags):
     flat = rt.FlatScene(np.array(c), np.array(r), mi, mats)
     lin, st = assert_parity(renderer, flat, cam_for(48, 27), 50, 8, flags)
     assert st.ray_segments > 48 * 27 * 8
+
+
+# ---- camera-batch cone cull (camera_sweep): never changes a result ----
+
+@pytest.mark.parametrize("w,h,vfov,spp", [(1, 1, 150.0, 100), (3, 2, 150.0, 40), (5, 3, 100.0, 100), (7, 5, 30.0, 36)])
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32, abi.RT_FLAG_MODE_SCALAR | abi.RT_FLAG_F32])
+def test_cone_cull_wide_pixels(renderer, scene_100, w, h, vfov, spp, flags):
+    """Tiny images with wide fields of view: a pixel spans tens of degrees, so some camera batches
+    exceed the cull's 30-degree cone and test every sphere, others cull with a wide cone; spp not a
+    multiple of 64 makes batches straddle two pixels (one cone over both)."""
+    cam = _cam(w, h, view_angle=vfov)
+    assert_parity(renderer, scene_100, cam, 50, spp, flags)
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32, abi.RT_FLAG_ROOT2 | abi.RT_FLAG_F32])
+def test_cone_cull_dense_tiny_spheres(renderer, flags):
+    """3000 spheres with radii 1e-3..0.1 scattered through the view frustum, many grazing the
+    primary rays of neighbouring pixels: the cull's margin must keep every sphere the reference's
+    arithmetic hits (bit parity with the oracle, every pixel)."""
+    rng = np.random.default_rng(17)
+    n = 3000
+    o = np.array(rt.MAIN_CAMERA["center"])
+    fwd = -o / np.linalg.norm(o)
+    up = np.array([0.0, 1.0, 0.0])
+    right = np.cross(fwd, up); right /= np.linalg.norm(right)
+    up2 = np.cross(right, fwd)
+    dist = rng.uniform(3.0, 40.0, n)
+    x = rng.uniform(-0.28, 0.28, n) * dist
+    y = rng.uniform(-0.16, 0.16, n) * dist
+    c = o + dist[:, None] * fwd + x[:, None] * right + y[:, None] * up2
+    r = 10.0 ** rng.uniform(-3, -1, n)
+    mats = [rt.Lambertian((0.7, 0.6, 0.5)), rt.Metal((0.9, 0.9, 0.9), 0.1), rt.Dielectric(1.5, False)]
+    flat = rt.FlatScene(c, r, rng.integers(0, 3, n).astype(np.uint32), mats)
+    lin, st = assert_parity(renderer, flat, cam_for(64, 36), 8, 16, flags)
+    assert st.ray_segments > 64 * 36 * 16 * 1.05   # some primary rays really hit the cloud
