@@ -74,6 +74,7 @@ __device__ __forceinline__ SphGroup<T> load_group(const __attribute__((address_s
 }
 
 typedef float f2 __attribute__((ext_vector_type(2)));
+struct Q4 { uint32_t x, y, z, w; };
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 template <typename T> struct KParams {
@@ -104,6 +105,14 @@ template <typename T> struct KParams {
     float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
     const float* cull;         // camera cone-cull table: {wx, wy, wz, rp} per sphere (build_cam_table)
     const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
+    // general sweep, two-level (build_layout / pack_sweep): slot-order exact and filter streams,
+    // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), per-cluster group ranges, slot -> scene index
+    const T* rsph;
+    const float* rfsph;
+    const float* ftop;
+    const uint32_t* tmeta;
+    const uint32_t* ridx;
+    uint32_t n_top;
 };
 
 constexpr int kSegShards = 256;
@@ -234,6 +243,39 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
     return (__float_as_uint(t0.x) | __float_as_uint(t0.y) | __float_as_uint(t1.x)) | __float_as_uint(t1.y);
 }
 
+// The general sweep's cluster test for one top group of 4 cluster bounds (same arithmetic and
+// per-lane constants as filter_group, with R2 for r2f); returns the 4-bit wave mask of clusters
+// that pass for some lane.
+__device__ __forceinline__ uint32_t cluster_mask(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3) {
+    const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
+    const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
+    f2 a0, b0, a1, b1, r0, r1;
+    asm volatile(
+        "v_pk_fma_f32 %[a0], %[cz0], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
+        "v_pk_fma_f32 %[b0], %[cz0], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[a1], %[cz1], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
+        "v_pk_fma_f32 %[b1], %[cz1], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[a0], %[cx0], %[K0], %[a0] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b0], %[cy0], %[K1], %[b0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[a1], %[cx1], %[K0], %[a1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b1], %[cy1], %[K1], %[b1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[b0], %[cx0], %[K1], %[b0] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b1], %[cx1], %[K1], %[b1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[r0], %[b0], %[b0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[r1], %[b1], %[b1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[r0], %[a0], %[a0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+        : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
+        : [cx0] "s"(cx0), [cy0] "s"(cy0), [cz0] "s"(cz0), [rr0] "s"(rr0), [cx1] "s"(cx1), [cy1] "s"(cy1),
+          [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3));
+    // cluster k passes for a lane iff its D >= +0 (sign bit clear)
+    const uint32_t m0 = __ballot((int32_t)__float_as_uint(r0.x) >= 0) != 0ull ? 1u : 0u;
+    const uint32_t m1 = __ballot((int32_t)__float_as_uint(r0.y) >= 0) != 0ull ? 2u : 0u;
+    const uint32_t m2 = __ballot((int32_t)__float_as_uint(r1.x) >= 0) != 0ull ? 4u : 0u;
+    const uint32_t m3 = __ballot((int32_t)__float_as_uint(r1.y) >= 0) != 0ull ? 8u : 0u;
+    return (m0 | m1) | (m2 | m3);
+}
+
 // The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
 // index of the nearest valid hit (-1: the sky, :421-424) and its t.
 // SCALAR selects Sphere::hit + Scene::hit (objects.rs:216-247, ray_tracing.rs:231-235): no FMA,
@@ -243,7 +285,9 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
 // (build_cam_table): oc and c come precomputed, bit-identical to the per-ray values.
 // Sphere::hit_packed's root and PackedHitRecords::update (objects.rs:263-290, 140-155) for a
 // candidate whose discriminant is non-negative; SCALAR: Sphere::hit + Scene::hit's min_by_key
-// (objects.rs:227-234, ray_tracing.rs:231-235: the first minimum wins).
+// (objects.rs:227-234, ray_tracing.rs:231-235: the first minimum wins).  i is the scene index; ties
+// are broken by it (later wins, scalar: earlier wins), so the result does not depend on the order
+// in which spheres are visited (the general sweep visits them cluster by cluster).
 template <typename T, bool root2, bool SCALAR>
 __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_a, T& best_t, int& best) {
     if constexpr (SCALAR) {
@@ -253,7 +297,7 @@ __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_
             root = (-hb + sd) / a;
             if (!(root >= T(0.001) && root < T(INFINITY))) return;
         }
-        if (root < best_t) { best_t = root; best = (int)i; }
+        if (root < best_t || (root == best_t && (int)i < best)) { best_t = root; best = (int)i; }   // first wins
         return;
     }
     const T sd = sqrt(disc);
@@ -264,7 +308,7 @@ __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_
         root = (-hb + sd) * inv_a;                         // :271
         valid = root >= T(0.001) && root < T(INFINITY);
     }
-    if (valid && root <= best_t) { best_t = root; best = (int)i; }   // ties: later wins (:141)
+    if (valid && (root < best_t || (root == best_t && (int)i > best))) { best_t = root; best = (int)i; }   // ties: later wins (:141)
 }
 
 template <typename T, bool root2, bool SCALAR = false, bool CAMT = false>
@@ -425,9 +469,20 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // (host, diagnostics and tests) sets f_cmax = +inf (every lane degenerate, every group
         // exact) and sc = -inf in the camera filter table.
         const auto& qa = *cold_args<T>();
+#ifdef RT_EXP_FLAT_SWEEP
         cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.fsph, 64);
         cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.sph, 64);
         const uint32_t ngf = qa.n_fgroups;
+        auto sidx = [&](uint32_t g) -> Q4 { return Q4{4 * g, 4 * g + 1, 4 * g + 2, 4 * g + 3}; };
+#else
+        cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.rfsph, 64);
+        cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.rsph, 64);
+        auto sidx = [&](uint32_t g) -> Q4 {   // scene indices of slot group g (one s_load_dwordx4)
+            const auto& qi = *cold_args<T>();
+            cptr<uint32_t> ri = (cptr<uint32_t>)__builtin_assume_aligned(qi.ridx, 16);
+            return Q4{ri[4 * g], ri[4 * g + 1], ri[4 * g + 2], ri[4 * g + 3]};
+        };
+#endif
         const float fdx = (float)d.x, fdy = (float)d.y, fdz = (float)d.z;
         const float fox = (float)o.x, foy = (float)o.y, foz = (float)o.z;
         const float L = __builtin_fmaf(fdz, fdz, fdx * fdx);
@@ -478,11 +533,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         disc[q] = fma2(hb[q], hb[q], na * c);                         // :257
                     }
                 }
-                const uint32_t i0 = 4 * g;
-                if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, i0);
-                if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, i0 + 1);
-                if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, i0 + 2);
-                if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, i0 + 3);
+                const Q4 si = sidx(g);
+                if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, si.x);
+                if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, si.y);
+                if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, si.z);
+                if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, si.w);
             } else {
                 const SphGroup<T> c0 = load_group(fe, 2 * g), c1 = load_group(fe, 2 * g + 1);
                 T hb[4], disc[4];
@@ -499,15 +554,53 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
                     }
                 }
+                const Q4 si = sidx(g);
+                const uint32_t sv[4] = {si.x, si.y, si.z, si.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    if (cand_f(hb[j], disc[j])) hit(hb[j], disc[j], 4 * g + j);
+                    if (cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
             }
         };
+#ifdef RT_EXP_FLAT_SWEEP
         auto group = [&](const SphGroup<float>& cur, uint32_t g) {
             if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g);
         };
         sphere_loop(ff, ngf, group);
+#else
+        // Two levels: a top group holds the bounds of 4 spatial clusters (build_layout); the lanes'
+        // filter against the bounds gives the clusters some lane may hit, and only their groups run
+        // the per-sphere filter (and, where it passes, the exact test).  A cluster bound contains its
+        // members, so the cluster filter passes whenever a member's filter would.  The next top group
+        // is requested before the current one's clusters are walked (their group loads wait for it).
+        cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 64);
+        cptr<uint32_t> tm = (cptr<uint32_t>)__builtin_assume_aligned(qa.tmeta, 16);
+        auto meta4 = [&](uint32_t t) -> Q4 { return Q4{tm[4 * t], tm[4 * t + 1], tm[4 * t + 2], tm[4 * t + 3]}; };
+        const uint32_t ntop = qa.n_top;
+        SphGroup<float> A = load_group(ft, 0);
+        Q4 M = meta4(0);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        for (uint32_t tg = 0; tg < ntop; ++tg) {
+            uint32_t pm = cluster_mask(A, K0, K1, K2, K3);
+            const Q4 Mc = M;
+            __builtin_amdgcn_sched_barrier(0);
+            A = load_group(ft, tg + 1);   // the stream holds one empty top group past the end
+            M = meta4(tg + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            while (pm != 0u) {
+                const uint32_t k = __builtin_ctz(pm);
+                pm &= pm - 1u;
+                const uint32_t mk4 = k == 0 ? Mc.x : k == 1 ? Mc.y : k == 2 ? Mc.z : Mc.w;
+                const uint32_t g0 = mk4 >> 3;
+                auto group = [&](const SphGroup<float>& cur, uint32_t g) {
+                    if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
+                };
+                sphere_loop(ff + 16u * g0, mk4 & 7u, group);
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
     }
     t_out = best_t;
     return best;
@@ -1239,6 +1332,11 @@ struct rt_context {
     void* camx64 = nullptr; void* camx32 = nullptr; // per-sphere camera-origin records (rebuilt per launch)
     void* cull64 = nullptr; void* cull32 = nullptr; // camera cone-cull records (fp32; rebuilt per launch)
     uint32_t n_cull = 0;                            // records: n_spheres rounded up to 64, + 64 padding
+    void* rsph64 = nullptr; void* rsph32 = nullptr; // general sweep: slot-order exact groups
+    void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
+    void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
+    uint32_t* tmeta = nullptr; uint32_t* ridx = nullptr;
+    uint32_t n_top = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
     uint32_t* smat = nullptr;
@@ -1323,6 +1421,11 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->cen64); (void)hipFree(c->cen32);
     (void)hipFree(c->camx64); (void)hipFree(c->camx32); (void)hipFree(c->cull64); (void)hipFree(c->cull32);
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
+    (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
+    (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->tmeta); (void)hipFree(c->ridx);
+    c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
+    c->tmeta = c->ridx = nullptr;
+    c->n_top = 0;
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
@@ -1387,7 +1490,7 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
 // other spheres: max |c|_1 (rounded up) and max r2f.
 template <typename T>
 static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float>& grp, uint32_t& n_fgroups,
-                        float& cmax, float& r2max, float& r2min) {
+                        float& cmax, float& r2max, float& r2min, std::vector<float>& frec) {
     n_fgroups = (n + 3) / 4;
     std::vector<double> key(n);
     for (uint32_t i = 0; i < n; ++i)
@@ -1421,6 +1524,7 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
     double rmin = std::numeric_limits<double>::infinity();
     cm = 0.0; rm = 0.0;
     grp.assign((size_t)16 * (n_fgroups + 1), 0.0f);
+    frec.assign((size_t)4 * n, 0.0f);
     for (uint32_t i = 0; i < 4 * (n_fgroups + 1); ++i) {
         float f[4] = {0.0f, 0.0f, 0.0f, -std::numeric_limits<float>::infinity()};
         if (i < n) {
@@ -1439,10 +1543,157 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
         }
         const uint32_t g = i / 4, j = i % 4;
         for (int q = 0; q < 4; ++q) grp[(size_t)16 * g + 8 * (j / 2) + 2 * q + (j % 2)] = f[q];   // pair-interleaved
+        if (i < n) for (int q = 0; q < 4; ++q) frec[(size_t)4 * i + q] = f[q];
     }
     cmax = up32(cm);
     r2max = up32(rm);
     r2min = std::isfinite(rmin) ? (float)rmin : 0.0f;   // exact: rmin is an fp32 value
+}
+
+// Spatial clusters for the general sweep's two-level filter (nearest_hit).  The filterable spheres
+// are split k-d style (median along the longest extent of the centres) into clusters of at most
+// kClusterMax spheres; the "always exact" ones (pack_filter) are chunked in scene order.  Each
+// cluster's spheres occupy whole 4-sphere groups of the slot-order streams (dummy-padded), and
+// clusters are padded to whole top groups of 4 (empty clusters, never taken).  The sweep visits
+// clusters in slot order, not scene order: hit_update's tie rule (equal t -> the later scene index
+// wins; scalar mode: the earlier) makes the nearest hit independent of the visiting order.
+constexpr uint32_t kClusterMax = 16;
+struct SweepLayout {
+    std::vector<int32_t> slot;                   // slot -> scene index, -1 = dummy (4 slots per group)
+    std::vector<std::vector<uint32_t>> members;  // per cluster (padded to a multiple of 4)
+    std::vector<uint32_t> meta;                  // per cluster: first group << 3 | groups (0: empty)
+};
+static SweepLayout build_layout(const rt_scene* s) {
+    const uint32_t n = s->n_spheres;
+    std::vector<double> key(n);
+    for (uint32_t i = 0; i < n; ++i)
+        key[i] = std::fabs(s->center[3 * i]) + std::fabs(s->center[3 * i + 1]) + std::fabs(s->center[3 * i + 2]) +
+                 std::fabs(s->radius[i]);
+    double median = 0.0;
+    if (n) {
+        std::vector<double> k2 = key;
+        std::nth_element(k2.begin(), k2.begin() + n / 2, k2.end());
+        median = k2[n / 2];
+    }
+    std::vector<uint32_t> filt, exact;
+    for (uint32_t i = 0; i < n; ++i) {
+        const bool fin = std::isfinite(key[i]) && std::isfinite(s->radius[i] * s->radius[i]);
+        (fin && !(key[i] > kExactRatio * median) ? filt : exact).push_back(i);
+    }
+    SweepLayout L;
+    std::vector<std::vector<uint32_t>> cl;
+    // k-d split; the left part takes a multiple of kClusterMax so that leaves stay full
+    std::vector<std::pair<size_t, size_t>> work{{0, filt.size()}};
+    while (!work.empty()) {
+        const auto [b, e] = work.back();
+        work.pop_back();
+        if (e - b <= kClusterMax) {
+            if (e > b) cl.emplace_back(filt.begin() + b, filt.begin() + e);
+            continue;
+        }
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = b; k < e; ++k)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], s->center[3 * filt[k] + a]);
+                hi[a] = std::max(hi[a], s->center[3 * filt[k] + a]);
+            }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        const size_t m = b + std::min(e - b - 1, (e - b + 2 * kClusterMax - 1) / (2 * kClusterMax) * kClusterMax);
+        std::nth_element(filt.begin() + b, filt.begin() + m, filt.begin() + e, [&](uint32_t x, uint32_t y) {
+            const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
+            return cx < cy || (cx == cy && x < y);
+        });
+        work.push_back({m, e});
+        work.push_back({b, m});
+    }
+    for (size_t k = 0; k < exact.size(); k += kClusterMax)
+        cl.emplace_back(exact.begin() + k, exact.begin() + std::min(exact.size(), k + kClusterMax));
+    while (cl.size() % 4) cl.emplace_back();
+    for (auto& c : cl) {
+        std::sort(c.begin(), c.end());
+        const uint32_t g0 = (uint32_t)(L.slot.size() / 4), ng = (uint32_t)((c.size() + 3) / 4);
+        for (uint32_t k = 0; k < 4 * ng; ++k) L.slot.push_back(k < c.size() ? (int32_t)c[k] : -1);
+        L.meta.push_back(ng ? (g0 << 3) | ng : 0u);
+    }
+    L.members = std::move(cl);
+    return L;
+}
+
+// Slot-order streams for rays in precision T: the exact groups (SphGroup layout of pack_scene),
+// the fp32 filter groups (pack_filter's records) and the top stream of cluster bounds, fp32 groups
+// of 4 {cx, cy, cz, R2}: the mean of the members' fp32 centres and R2 >= (max |c_i - C| + r_i)^2
+// (r_i from the member's filter r2f, so the floor applies), inflated by 2^-20 relative and 4 u |.|_1
+// for the fp32 rounding of C; +inf if any member is always exact, -inf for an empty cluster.  The
+// bounds enter the margin maxima (cmax, r2max) like spheres; r2min is unchanged (R2 >= any member r2f).
+template <typename T>
+static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec, const SweepLayout& L,
+                       std::vector<T>& rgrp, std::vector<float>& rfgrp, std::vector<float>& top, float& cmax,
+                       float& r2max) {
+    auto up32 = [](double v) -> float {
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+        return f;
+    };
+    const size_t ns = L.slot.size(), nfg = ns / 4;
+    constexpr uint32_t G = kGroup<T>, NE = 64 / sizeof(T);
+    rgrp.assign((size_t)NE * (ns / G + 1), T(0));
+    rfgrp.assign((size_t)16 * (nfg + 1), 0.0f);
+    for (size_t i = 0; i < ns + G; ++i) {   // exact groups, + one dummy group
+        const int32_t sc = i < ns ? L.slot[i] : -1;
+        const size_t g = i / G, j = i % G;
+        for (int f = 0; f < 4; ++f) {
+            T v = f == 3 ? -std::numeric_limits<T>::infinity() : T(0);
+            if (sc >= 0) v = f == 3 ? cen[4 * sc + 3] * cen[4 * sc + 3] : cen[4 * sc + f];   // r.powi(2) in T
+            if (sizeof(T) == 4) rgrp[g * NE + 8 * (j / 2) + 2 * f + (j % 2)] = v;
+            else rgrp[g * NE + 4 * j + f] = v;
+        }
+    }
+    for (size_t i = 0; i < ns + 4; ++i) {   // filter groups, + one dummy group (prefetch target)
+        const int32_t sc = i < ns ? L.slot[i] : -1;
+        for (int f = 0; f < 4; ++f) {
+            const float fv = sc >= 0 ? frec[(size_t)4 * sc + f] : (f == 3 ? -INFINITY : 0.0f);
+            rfgrp[(size_t)16 * (i / 4) + 8 * ((i % 4) / 2) + 2 * f + (i % 2)] = fv;
+        }
+    }
+    const size_t nc = L.members.size();
+    top.assign((size_t)4 * (nc + 4), 0.0f);   // + one empty top group (prefetch target)
+    double cm = cmax, rm = r2max;
+    for (size_t k = 0; k < nc + 4; ++k) {
+        float b[4] = {0.0f, 0.0f, 0.0f, -INFINITY};
+        if (k < nc && !L.members[k].empty()) {
+            const auto& m = L.members[k];
+            double C[3] = {0, 0, 0};
+            bool inf = false;
+            for (uint32_t i : m) {
+                for (int a = 0; a < 3; ++a) C[a] += (double)frec[4 * i + a];
+                if (!(frec[4 * i + 3] < INFINITY)) inf = true;
+            }
+            for (int a = 0; a < 3; ++a) b[a] = (float)(C[a] / (double)m.size());
+            if (inf) {
+                b[3] = INFINITY;
+            } else {
+                double R = 0.0, r2m = 0.0, c1 = 0.0;
+                for (uint32_t i : m) {
+                    const double dx = frec[4 * i] - (double)b[0], dy = frec[4 * i + 1] - (double)b[1],
+                                 dz = frec[4 * i + 2] - (double)b[2];
+                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::sqrt((double)frec[4 * i + 3]));
+                    r2m = std::max(r2m, (double)frec[4 * i + 3]);
+                    c1 = std::max(c1, std::fabs((double)frec[4 * i]) + std::fabs((double)frec[4 * i + 1]) +
+                                          std::fabs((double)frec[4 * i + 2]));
+                }
+                const double cb = std::fabs((double)b[0]) + std::fabs((double)b[1]) + std::fabs((double)b[2]);
+                R = R * (1.0 + 0x1.0p-20) + 0x1.0p-22 * (cb + c1);
+                b[3] = up32(std::max(R * R, r2m));
+                cm = std::max(cm, cb);
+                rm = std::max(rm, (double)b[3]);
+            }
+        }
+        const size_t tg = k / 4, j = k % 4;
+        for (int f = 0; f < 4; ++f) top[16 * tg + 8 * (j / 2) + 2 * f + (j % 2)] = b[f];
+    }
+    cmax = up32(cm);
+    r2max = up32(rm);
 }
 
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
@@ -1473,12 +1724,28 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     if ((rc = up(&c->sph64, g64.data(), g64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->sph32, g32.data(), g32.size() * sizeof(float))) != RT_OK) return rc;
     {
-        std::vector<float> f64g, f32g;
+        std::vector<float> f64g, f32g, fr64, fr32;
         uint32_t nf = 0;
-        pack_filter(c64, s->n_spheres, f64g, nf, c->f_cmax64, c->f_r2max64, c->f_r2min64);
-        pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32, c->f_r2min32);
+        pack_filter(c64, s->n_spheres, f64g, nf, c->f_cmax64, c->f_r2max64, c->f_r2min64, fr64);
+        pack_filter(c32, s->n_spheres, f32g, c->n_fgroups, c->f_cmax32, c->f_r2max32, c->f_r2min32, fr32);
         if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
+        const SweepLayout L = build_layout(s);
+        std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32;
+        pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64);
+        pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32);
+        std::vector<uint32_t> ridx(L.slot.size() + 4, 0u), meta(L.meta);
+        for (size_t i = 0; i < L.slot.size(); ++i) ridx[i] = L.slot[i] < 0 ? 0u : (uint32_t)L.slot[i];
+        meta.resize(meta.size() + 4, 0u);   // the empty prefetch top group
+        c->n_top = (uint32_t)(L.meta.size() / 4);
+        if ((rc = up(&c->rsph64, rg64.data(), rg64.size() * sizeof(double))) != RT_OK) return rc;
+        if ((rc = up(&c->rsph32, rg32.data(), rg32.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->rfsph64, rf64.data(), rf64.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->rfsph32, rf32.data(), rf32.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->top64, t64.data(), t64.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->top32, t32.data(), t32.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up((void**)&c->ridx, ridx.data(), ridx.size() * sizeof(uint32_t))) != RT_OK) return rc;
+        if ((rc = up((void**)&c->tmeta, meta.data(), meta.size() * sizeof(uint32_t))) != RT_OK) return rc;
         HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
         HIPCHK(hipMalloc(&c->camf32, f32g.size() * sizeof(float)));
     }
@@ -1533,6 +1800,12 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_groups = f64 ? c->n_groups64 : c->n_groups32;
     p.fsph = (const float*)(f64 ? c->fsph64 : c->fsph32);
     p.n_fgroups = c->n_fgroups;
+    p.rsph = (const T*)(f64 ? c->rsph64 : c->rsph32);
+    p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
+    p.ftop = (const float*)(f64 ? c->top64 : c->top32);
+    p.tmeta = c->tmeta;
+    p.ridx = c->ridx;
+    p.n_top = c->n_top;
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
     p.f_r2min = f64 ? c->f_r2min64 : c->f_r2min32;
