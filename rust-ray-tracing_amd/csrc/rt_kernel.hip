@@ -106,13 +106,13 @@ template <typename T> struct KParams {
     const float* cull;         // camera cone-cull table: {wx, wy, wz, rp} per sphere (build_cam_table)
     const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
     // general sweep, two-level (build_layout / pack_sweep): slot-order exact and filter streams,
-    // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), per-cluster group ranges, slot -> scene index
+    // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), slot -> scene index; n_top top groups,
+    // n_xg leading groups of always-exact spheres, then cluster k at groups n_xg + 4k .. + 3
     const T* rsph;
     const float* rfsph;
     const float* ftop;
-    const uint32_t* tmeta;
     const uint32_t* ridx;
-    uint32_t n_top;
+    uint32_t n_top, n_xg;
 };
 
 constexpr int kSegShards = 256;
@@ -567,38 +567,27 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         };
         sphere_loop(ff, ngf, group);
 #else
-        // Two levels: a top group holds the bounds of 4 spatial clusters (build_layout); the lanes'
-        // filter against the bounds gives the clusters some lane may hit, and only their groups run
-        // the per-sphere filter (and, where it passes, the exact test).  A cluster bound contains its
-        // members, so the cluster filter passes whenever a member's filter would.  The next top group
-        // is requested before the current one's clusters are walked (their group loads wait for it).
+        // Two levels (build_layout): the always-exact spheres first, then spatial clusters of 16
+        // spheres (4 groups each) with bounding spheres, 4 bounds per top group.  Per chunk of 32
+        // clusters: phase 1 tests the bounds with the lanes' filter (a cluster bound contains its
+        // members, so it passes whenever a member's filter would) into a 32-bit wave mask; phase 2
+        // walks the set clusters' groups with the per-sphere filter and, where it passes, the exact
+        // test.  The phases never hold both SGPR pipelines at once (no SGPR spills).
+        const uint32_t nxg = qa.n_xg, ntop = qa.n_top;
+        for (uint32_t g = 0; g < nxg; ++g) exact4(g);
         cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 64);
-        cptr<uint32_t> tm = (cptr<uint32_t>)__builtin_assume_aligned(qa.tmeta, 16);
-        auto meta4 = [&](uint32_t t) -> Q4 { return Q4{tm[4 * t], tm[4 * t + 1], tm[4 * t + 2], tm[4 * t + 3]}; };
-        const uint32_t ntop = qa.n_top;
-        SphGroup<float> A = load_group(ft, 0);
-        Q4 M = meta4(0);
-        __builtin_amdgcn_s_waitcnt(0xC07F);
-        __builtin_amdgcn_sched_barrier(0);
-        for (uint32_t tg = 0; tg < ntop; ++tg) {
-            uint32_t pm = cluster_mask(A, K0, K1, K2, K3);
-            const Q4 Mc = M;
-            __builtin_amdgcn_sched_barrier(0);
-            A = load_group(ft, tg + 1);   // the stream holds one empty top group past the end
-            M = meta4(tg + 1);
-            __builtin_amdgcn_sched_barrier(0);
-            while (pm != 0u) {
-                const uint32_t k = __builtin_ctz(pm);
-                pm &= pm - 1u;
-                const uint32_t mk4 = k == 0 ? Mc.x : k == 1 ? Mc.y : k == 2 ? Mc.z : Mc.w;
-                const uint32_t g0 = mk4 >> 3;
-                auto group = [&](const SphGroup<float>& cur, uint32_t g) {
+        for (uint32_t t0 = 0; t0 < ntop; t0 += 8u) {
+            uint32_t mask = 0;
+            sphere_loop(ft + 16u * t0, min(8u, ntop - t0), [&](const SphGroup<float>& cur, uint32_t t) {
+                mask |= cluster_mask(cur, K0, K1, K2, K3) << (4u * t);
+            });
+            while (mask != 0u) {
+                const uint32_t g0 = nxg + 4u * (4u * t0 + (uint32_t)__builtin_ctz(mask));
+                mask &= mask - 1u;
+                sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                     if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
-                };
-                sphere_loop(ff + 16u * g0, mk4 & 7u, group);
+                });
             }
-            __builtin_amdgcn_s_waitcnt(0xC07F);
-            __builtin_amdgcn_sched_barrier(0);
         }
 #endif
     }
@@ -1335,8 +1324,8 @@ struct rt_context {
     void* rsph64 = nullptr; void* rsph32 = nullptr; // general sweep: slot-order exact groups
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
-    uint32_t* tmeta = nullptr; uint32_t* ridx = nullptr;
-    uint32_t n_top = 0;
+    uint32_t* ridx = nullptr;
+    uint32_t n_top = 0, n_xg = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
     uint32_t* smat = nullptr;
@@ -1422,10 +1411,10 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->camx64); (void)hipFree(c->camx32); (void)hipFree(c->cull64); (void)hipFree(c->cull32);
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
-    (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->tmeta); (void)hipFree(c->ridx);
+    (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
     c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
-    c->tmeta = c->ridx = nullptr;
-    c->n_top = 0;
+    c->ridx = nullptr;
+    c->n_top = c->n_xg = 0;
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
@@ -1550,18 +1539,19 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
     r2min = std::isfinite(rmin) ? (float)rmin : 0.0f;   // exact: rmin is an fp32 value
 }
 
-// Spatial clusters for the general sweep's two-level filter (nearest_hit).  The filterable spheres
-// are split k-d style (median along the longest extent of the centres) into clusters of at most
-// kClusterMax spheres; the "always exact" ones (pack_filter) are chunked in scene order.  Each
-// cluster's spheres occupy whole 4-sphere groups of the slot-order streams (dummy-padded), and
-// clusters are padded to whole top groups of 4 (empty clusters, never taken).  The sweep visits
-// clusters in slot order, not scene order: hit_update's tie rule (equal t -> the later scene index
-// wins; scalar mode: the earlier) makes the nearest hit independent of the visiting order.
+// Spatial clusters for the general sweep's two-level filter (nearest_hit).  Slot order: first the
+// "always exact" spheres (pack_filter's rule: non-finite, or |c|_1 + r above 8x the median, e.g. a
+// ground sphere) in scene order, padded to whole groups -- every ray tests them exactly; then the
+// filterable spheres, split k-d style (median along the longest extent of the centres) into
+// clusters of at most kClusterMax = 16 spheres, each cluster in 4 whole groups (dummy-padded).  The
+// cluster count is padded to whole top groups of 4 with empty clusters (never taken).  The sweep
+// visits spheres in slot order, not scene order: hit_update's tie rule (equal t -> the later scene
+// index wins; scalar mode: the earlier) makes the nearest hit independent of the visiting order.
 constexpr uint32_t kClusterMax = 16;
 struct SweepLayout {
     std::vector<int32_t> slot;                   // slot -> scene index, -1 = dummy (4 slots per group)
-    std::vector<std::vector<uint32_t>> members;  // per cluster (padded to a multiple of 4)
-    std::vector<uint32_t> meta;                  // per cluster: first group << 3 | groups (0: empty)
+    std::vector<std::vector<uint32_t>> members;  // per cluster (count padded to a multiple of 4)
+    uint32_t n_xg = 0;                           // leading groups of always-exact spheres
 };
 static SweepLayout build_layout(const rt_scene* s) {
     const uint32_t n = s->n_spheres;
@@ -1581,14 +1571,16 @@ static SweepLayout build_layout(const rt_scene* s) {
         (fin && !(key[i] > kExactRatio * median) ? filt : exact).push_back(i);
     }
     SweepLayout L;
-    std::vector<std::vector<uint32_t>> cl;
+    for (uint32_t i : exact) L.slot.push_back((int32_t)i);
+    while (L.slot.size() % 4) L.slot.push_back(-1);
+    L.n_xg = (uint32_t)(L.slot.size() / 4);
     // k-d split; the left part takes a multiple of kClusterMax so that leaves stay full
     std::vector<std::pair<size_t, size_t>> work{{0, filt.size()}};
     while (!work.empty()) {
         const auto [b, e] = work.back();
         work.pop_back();
         if (e - b <= kClusterMax) {
-            if (e > b) cl.emplace_back(filt.begin() + b, filt.begin() + e);
+            if (e > b) L.members.emplace_back(filt.begin() + b, filt.begin() + e);
             continue;
         }
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -1607,16 +1599,11 @@ static SweepLayout build_layout(const rt_scene* s) {
         work.push_back({m, e});
         work.push_back({b, m});
     }
-    for (size_t k = 0; k < exact.size(); k += kClusterMax)
-        cl.emplace_back(exact.begin() + k, exact.begin() + std::min(exact.size(), k + kClusterMax));
-    while (cl.size() % 4) cl.emplace_back();
-    for (auto& c : cl) {
+    while (L.members.size() % 4) L.members.emplace_back();
+    for (auto& c : L.members) {
         std::sort(c.begin(), c.end());
-        const uint32_t g0 = (uint32_t)(L.slot.size() / 4), ng = (uint32_t)((c.size() + 3) / 4);
-        for (uint32_t k = 0; k < 4 * ng; ++k) L.slot.push_back(k < c.size() ? (int32_t)c[k] : -1);
-        L.meta.push_back(ng ? (g0 << 3) | ng : 0u);
+        for (uint32_t k = 0; k < kClusterMax; ++k) L.slot.push_back(k < c.size() ? (int32_t)c[k] : -1);
     }
-    L.members = std::move(cl);
     return L;
 }
 
@@ -1734,10 +1721,10 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32;
         pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64);
         pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32);
-        std::vector<uint32_t> ridx(L.slot.size() + 4, 0u), meta(L.meta);
+        std::vector<uint32_t> ridx(L.slot.size() + 4, 0u);
         for (size_t i = 0; i < L.slot.size(); ++i) ridx[i] = L.slot[i] < 0 ? 0u : (uint32_t)L.slot[i];
-        meta.resize(meta.size() + 4, 0u);   // the empty prefetch top group
-        c->n_top = (uint32_t)(L.meta.size() / 4);
+        c->n_top = (uint32_t)(L.members.size() / 4);
+        c->n_xg = L.n_xg;
         if ((rc = up(&c->rsph64, rg64.data(), rg64.size() * sizeof(double))) != RT_OK) return rc;
         if ((rc = up(&c->rsph32, rg32.data(), rg32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->rfsph64, rf64.data(), rf64.size() * sizeof(float))) != RT_OK) return rc;
@@ -1745,7 +1732,6 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->top64, t64.data(), t64.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->top32, t32.data(), t32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up((void**)&c->ridx, ridx.data(), ridx.size() * sizeof(uint32_t))) != RT_OK) return rc;
-        if ((rc = up((void**)&c->tmeta, meta.data(), meta.size() * sizeof(uint32_t))) != RT_OK) return rc;
         HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
         HIPCHK(hipMalloc(&c->camf32, f32g.size() * sizeof(float)));
     }
@@ -1803,9 +1789,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.rsph = (const T*)(f64 ? c->rsph64 : c->rsph32);
     p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
     p.ftop = (const float*)(f64 ? c->top64 : c->top32);
-    p.tmeta = c->tmeta;
     p.ridx = c->ridx;
     p.n_top = c->n_top;
+    p.n_xg = c->n_xg;
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
     p.f_r2min = f64 ? c->f_r2min64 : c->f_r2min32;
