@@ -126,7 +126,7 @@ constexpr double kExactRatio = 8.0;  // spheres with |c|_1 + r > kExactRatio x t
 
 // Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..6.
 #ifdef RT_KSTATS
-__shared__ unsigned long long g_kst[4][4];
+__shared__ unsigned long long g_kst[4][8];
 __device__ __forceinline__ void kstat(uint32_t i, uint32_t n = 1) {
     const unsigned long long ex = __builtin_amdgcn_read_exec();
     if ((threadIdx.x & 63u) == (uint32_t)__builtin_ctzll(ex)) atomicAdd(&g_kst[threadIdx.x >> 6][i], (unsigned long long)n);
@@ -243,10 +243,13 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
     return (__float_as_uint(t0.x) | __float_as_uint(t0.y) | __float_as_uint(t1.x)) | __float_as_uint(t1.y);
 }
 
-// The general sweep's cluster test for one top group of 4 cluster bounds (same arithmetic and
-// per-lane constants as filter_group, with R2 for r2f); returns the 4-bit wave mask of clusters
-// that pass for some lane.
-__device__ __forceinline__ uint32_t cluster_mask(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3) {
+// The general sweep's cluster test for one top group of 4 cluster bounds {C, R2}: the line test of
+// filter_group (same per-lane constants K0..K3, R2 for r2f) and a "behind" test: with h = d^ sg
+// and t = C.h - o.h + 16 u pm (K4 = {hx, hy}, K5 = {hz, -(o.h) + 16 u pm}), a cluster entirely
+// behind the ray's origin (t < 0 and t^2 > R2) cannot hold a hit at root >= 0.001 > 0.  Returns the
+// 4-bit wave mask of clusters that pass both tests for some lane.
+__device__ __forceinline__ uint32_t cluster_mask(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3, f2 K4,
+                                                 f2 K5) {
     const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
     const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
     f2 a0, b0, a1, b1, r0, r1;
@@ -264,15 +267,27 @@ __device__ __forceinline__ uint32_t cluster_mask(const SphGroup<float>& cur, f2 
         "v_pk_fma_f32 %[r0], %[b0], %[b0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
         "v_pk_fma_f32 %[r1], %[b1], %[b1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
         "v_pk_fma_f32 %[r0], %[a0], %[a0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
+        "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %[a0], %[cz0], %[K5], %[K5] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"   // t = cz*hz - o.h'
+        "v_pk_fma_f32 %[a1], %[cz1], %[K5], %[K5] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[a0], %[cy0], %[K4], %[a0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"   // + cy*hy
+        "v_pk_fma_f32 %[a1], %[cy1], %[K4], %[a1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[a0], %[cx0], %[K4], %[a0] op_sel_hi:[1,0,1]\n\t"                  // + cx*hx
+        "v_pk_fma_f32 %[a1], %[cx1], %[K4], %[a1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[b0], %[a0], %[a0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"      // q = R2 - t^2
+        "v_pk_fma_f32 %[b1], %[a1], %[a1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
         : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
         : [cx0] "s"(cx0), [cy0] "s"(cy0), [cz0] "s"(cz0), [rr0] "s"(rr0), [cx1] "s"(cx1), [cy1] "s"(cy1),
-          [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3));
-    // cluster k passes for a lane iff its D >= +0 (sign bit clear)
-    const uint32_t m0 = __ballot((int32_t)__float_as_uint(r0.x) >= 0) != 0ull ? 1u : 0u;
-    const uint32_t m1 = __ballot((int32_t)__float_as_uint(r0.y) >= 0) != 0ull ? 2u : 0u;
-    const uint32_t m2 = __ballot((int32_t)__float_as_uint(r1.x) >= 0) != 0ull ? 4u : 0u;
-    const uint32_t m3 = __ballot((int32_t)__float_as_uint(r1.y) >= 0) != 0ull ? 8u : 0u;
+          [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3), [K4] "v"(K4),
+          [K5] "v"(K5));
+    // culled iff sign(D) | (sign(t) & sign(q)); cluster k passes for a lane iff that sign is clear
+    auto cull = [](float D, float t, float q) -> int32_t {
+        return (int32_t)(__float_as_uint(D) | (__float_as_uint(t) & __float_as_uint(q)));
+    };
+    const uint32_t m0 = __ballot(cull(r0.x, a0.x, b0.x) >= 0) != 0ull ? 1u : 0u;
+    const uint32_t m1 = __ballot(cull(r0.y, a0.y, b0.y) >= 0) != 0ull ? 2u : 0u;
+    const uint32_t m2 = __ballot(cull(r1.x, a1.x, b1.x) >= 0) != 0ull ? 4u : 0u;
+    const uint32_t m3 = __ballot(cull(r1.y, a1.y, b1.y) >= 0) != 0ull ? 8u : 0u;
     return (m0 | m1) | (m2 | m3);
 }
 
@@ -500,13 +515,20 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         float oe2 = __builtin_fmaf(foz, e2z, __builtin_fmaf(foy, e2y, fox * e2x));
         // Degenerate lanes: L*af must not underflow (L >= 1e-15: d within ~3e-8 of the y axis), and
         // x^2, y^2 must stay finite (|c|_1 + |o|_1 <= 1e15), so D is never inf - inf.
+        // Behind test of the cluster bounds (cluster_mask): h = d^ sg, and -(o.h) + 16 u pm, the margin
+        // covering the fp32 rounding of C.h - o.h (|C|_1 <= cmax).
+        const float sh = (1.0f / sqrtf(af)) * sg;
+        float hx = fdx * sh, hy = fdy * sh, hz = fdz * sh;
+        float noh = __builtin_fmaf(pm, 16.0f * 0x1.0p-24f, -__builtin_fmaf(foz, hz, __builtin_fmaf(foy, hy, fox * hx)));
         if (!(L >= 1e-15f) || !(pm <= 1e15f)) {   // zero basis: x = y = 0, every real sphere passes
             e1x = e1z = e2x = e2y = e2z = 0.0f;
             oe1 = oe2 = 0.0f;
+            hx = hy = hz = noh = 0.0f;
         }
         // Two per-lane constants per VGPR pair; every use broadcasts one half through the packed
         // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
         const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, 0.0f}, K3 = {-oe1, -oe2};
+        const f2 K4 = {hx, hy}, K5 = {hz, noh};
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222).
         auto exact4 = [&](uint32_t g) {
             KSTAT(0);
@@ -579,11 +601,13 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         for (uint32_t t0 = 0; t0 < ntop; t0 += 8u) {
             uint32_t mask = 0;
             sphere_loop(ft + 16u * t0, min(8u, ntop - t0), [&](const SphGroup<float>& cur, uint32_t t) {
-                mask |= cluster_mask(cur, K0, K1, K2, K3) << (4u * t);
+                KSTAT(5);
+                mask |= cluster_mask(cur, K0, K1, K2, K3, K4, K5) << (4u * t);
             });
             while (mask != 0u) {
                 const uint32_t g0 = nxg + 4u * (4u * t0 + (uint32_t)__builtin_ctz(mask));
                 mask &= mask - 1u;
+                KSTAT(4);
                 sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                     if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
                 });
@@ -1071,7 +1095,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
 #ifdef RT_KSTATS
-    if (lane < 4) g_kst[wave][lane] = 0;
+    if (lane < 8) g_kst[wave][lane] = 0;
 #endif
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u};
@@ -1154,6 +1178,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (lane == s) slot_left -= (uint32_t)__popcll(m);
             if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
                 if (!synced) { wave_mem_sync(); synced = true; }
+                KSTAT(6);
                 const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
                                                          s_hist[wave]);
                 if (lane == 0) wcount[wave][2] += K;
@@ -1284,7 +1309,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         atomicAdd(cc + 1, wcount[wave][1]);
         atomicAdd(cc + 2, wcount[wave][2]);
 #ifdef RT_KSTATS
-        for (int i = 0; i < 4; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);
+        for (int i = 0; i < 8; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);
 #endif
     }
 }
@@ -1933,12 +1958,15 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
     HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
     HIPCHK(hipMemset(c->err, 0, 16));
-    uint64_t total = 0, slots = 0, iters = 0, kst[4] = {0, 0, 0, 0};
+    uint64_t total = 0, slots = 0, iters = 0, kst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int i = 0; i < kSegShards; ++i)
-        for (int j = 0; j < 4; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
+        for (int j = 0; j < 8; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
     if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
-        fprintf(stderr, "rt_kstats: general taken_groups %llu sweeps %llu  camera taken_groups %llu sweeps %llu\n",
-                (unsigned long long)kst[0], (unsigned long long)kst[1], (unsigned long long)kst[2], (unsigned long long)kst[3]);
+        fprintf(stderr, "rt_kstats: general taken_groups %llu sweeps %llu clusters %llu top_groups %llu  camera "
+                "candidates %llu sweeps %llu  finish_pixel %llu\n",
+                (unsigned long long)kst[0], (unsigned long long)kst[1], (unsigned long long)kst[4],
+                (unsigned long long)kst[5], (unsigned long long)kst[2], (unsigned long long)kst[3],
+                (unsigned long long)kst[6]);
     for (int i = 0; i < kSegShards; ++i) {
         total += segs[(size_t)i * kSegStride];
         slots += segs[(size_t)i * kSegStride + 1];
