@@ -75,6 +75,17 @@ __device__ __forceinline__ SphGroup<T> load_group(const __attribute__((address_s
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 struct Q4 { uint32_t x, y, z, w; };
+
+// One top group of the general sweep: 4 cluster boxes {centre, half-extent} (pack_sweep), 96 bytes,
+// pair-interleaved like SphGroup: pair q at 12 q, {cx0,cx1, cy0,cy1, cz0,cz1, hx0,hx1, hy0,hy1, hz0,hz1}.
+constexpr uint32_t kBoxFloats = 24;
+struct alignas(32) BoxGroup { float v[kBoxFloats]; };
+__device__ __forceinline__ BoxGroup load_box(const __attribute__((address_space(4))) float* f, uint32_t g) {
+    BoxGroup r;
+#pragma unroll
+    for (uint32_t e = 0; e < kBoxFloats; ++e) r.v[e] = f[g * kBoxFloats + e];
+    return r;
+}
 __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 
 template <typename T> struct KParams {
@@ -117,7 +128,7 @@ template <typename T> struct KParams {
 
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
-constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep)
+constexpr int kWavesF32 = 5;   // default min-waves-per-SIMD targets (measured sweep)
 constexpr int kWavesF64 = 4;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
@@ -161,6 +172,28 @@ template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args_afte
 // next group's load is pinned (sched_barrier) BEFORE the current group's math and waited right
 // after it, so it is always one whole group of VALU work old when it is consumed.  The device
 // buffer holds a dummy group past the end, so the prefetches never need clamping.
+// The same two-deep pipeline over the general sweep's box groups (cluster bounds).
+template <typename F>
+__device__ __forceinline__ void box_loop(cptr<float> f, uint32_t ng, F&& group) {
+    BoxGroup A = load_box(f, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t g = 0;
+    for (; g + 1 < ng; g += 2) {
+        const BoxGroup B = load_box(f, g + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        group(A, g);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        A = load_box(f, g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        group(B, g + 1);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g < ng) group(A, g);
+}
+
 template <typename T, typename F>
 __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
     SphGroup<T> A = load_group(f, 0);
@@ -243,52 +276,41 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
     return (__float_as_uint(t0.x) | __float_as_uint(t0.y) | __float_as_uint(t1.x)) | __float_as_uint(t1.y);
 }
 
-// The general sweep's cluster test for one top group of 4 cluster bounds {C, R2}: the line test of
-// filter_group (same per-lane constants K0..K3, R2 for r2f) and a "behind" test: with h = d^ sg
-// and t = C.h - o.h + 16 u pm (K4 = {hx, hy}, K5 = {hz, -(o.h) + 16 u pm}), a cluster entirely
-// behind the ray's origin (t < 0 and t^2 > R2) cannot hold a hit at root >= 0.001 > 0.  Returns the
-// 4-bit wave mask of clusters that pass both tests for some lane.
-__device__ __forceinline__ uint32_t cluster_mask(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3, f2 K4,
-                                                 f2 K5) {
-    const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
-    const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
-    f2 a0, b0, a1, b1, r0, r1;
+// The general sweep's cluster test for one top group of 4 cluster boxes: a slab test of the ray
+// against each box widened by the lane's margin.  Per axis a: u = C.i + A (i = 1/d, A = -o.i), near
+// t = u - h J and far t = u + h J with J = |i| (1 + kappa) (nearest_hit), tn = max over axes of
+// near, tf = min of far; a cluster is culled for the lane iff tf < tn or tf < 0 (NaN: kept).
+// B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, -}, broadcast with op_sel;
+// 9 packed FMAs per box pair, then max3/min3 per box.  Returns the 4-bit wave mask of clusters
+// that pass for some lane.
+__device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
+    f2 ux, uy, uz, nx, ny, nz;
+    const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, hx = {v[6], v[7]}, hy = {v[8], v[9]},
+             hz = {v[10], v[11]};
+    // one pair at a time (12 temporaries); each packed result is read 3 instructions after its write
     asm volatile(
-        "v_pk_fma_f32 %[a0], %[cz0], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
-        "v_pk_fma_f32 %[b0], %[cz0], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[a1], %[cz1], %[K0], %[K3] op_sel:[0,1,0] op_sel_hi:[1,1,0]\n\t"
-        "v_pk_fma_f32 %[b1], %[cz1], %[K2], %[K3] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[a0], %[cx0], %[K0], %[a0] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[b0], %[cy0], %[K1], %[b0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[a1], %[cx1], %[K0], %[a1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[b1], %[cy1], %[K1], %[b1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[b0], %[cx0], %[K1], %[b0] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[b1], %[cx1], %[K1], %[b1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[r0], %[b0], %[b0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %[r1], %[b1], %[b1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %[r0], %[a0], %[a0], %[r0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %[r1], %[a1], %[a1], %[r1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %[a0], %[cz0], %[K5], %[K5] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"   // t = cz*hz - o.h'
-        "v_pk_fma_f32 %[a1], %[cz1], %[K5], %[K5] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[a0], %[cy0], %[K4], %[a0] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"   // + cy*hy
-        "v_pk_fma_f32 %[a1], %[cy1], %[K4], %[a1] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
-        "v_pk_fma_f32 %[a0], %[cx0], %[K4], %[a0] op_sel_hi:[1,0,1]\n\t"                  // + cx*hx
-        "v_pk_fma_f32 %[a1], %[cx1], %[K4], %[a1] op_sel_hi:[1,0,1]\n\t"
-        "v_pk_fma_f32 %[b0], %[a0], %[a0], %[rr0] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"      // q = R2 - t^2
-        "v_pk_fma_f32 %[b1], %[a1], %[a1], %[rr1] neg_lo:[1,0,0] neg_hi:[1,0,0]"
-        : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
-        : [cx0] "s"(cx0), [cy0] "s"(cy0), [cz0] "s"(cz0), [rr0] "s"(rr0), [cx1] "s"(cx1), [cy1] "s"(cy1),
-          [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3), [K4] "v"(K4),
-          [K5] "v"(K5));
-    // culled iff sign(D) | (sign(t) & sign(q)); cluster k passes for a lane iff that sign is clear
-    auto cull = [](float D, float t, float q) -> int32_t {
-        return (int32_t)(__float_as_uint(D) | (__float_as_uint(t) & __float_as_uint(q)));
+        "v_pk_fma_f32 %[ux], %[cx], %[B0], %[B2] op_sel_hi:[1,0,0]\n\t"                         // u = c i + A
+        "v_pk_fma_f32 %[uy], %[cy], %[B0], %[B2] op_sel:[0,1,1] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[uz], %[cz], %[B1], %[B1] op_sel:[0,0,1] op_sel_hi:[1,0,1]\n\t"
+        "v_pk_fma_f32 %[nx], %[hx], %[B3], %[ux] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]\n\t"   // near = u - h J
+        "v_pk_fma_f32 %[ny], %[hy], %[B3], %[uy] op_sel:[0,1,0] op_sel_hi:[1,1,1] neg_lo:[0,1,0] neg_hi:[0,1,0]\n\t"
+        "v_pk_fma_f32 %[nz], %[hz], %[B4], %[uz] op_sel_hi:[1,0,1] neg_lo:[0,1,0] neg_hi:[0,1,0]\n\t"
+        "v_pk_fma_f32 %[ux], %[hx], %[B3], %[ux] op_sel_hi:[1,0,1]\n\t"                        // far = u + h J
+        "v_pk_fma_f32 %[uy], %[hy], %[B3], %[uy] op_sel:[0,1,0] op_sel_hi:[1,1,1]\n\t"
+        "v_pk_fma_f32 %[uz], %[hz], %[B4], %[uz] op_sel_hi:[1,0,1]"
+        : [ux] "=&v"(ux), [uy] "=&v"(uy), [uz] "=&v"(uz), [nx] "=&v"(nx), [ny] "=&v"(ny), [nz] "=&v"(nz)
+        : [cx] "s"(cx), [cy] "s"(cy), [cz] "s"(cz), [hx] "s"(hx), [hy] "s"(hy), [hz] "s"(hz), [B0] "v"(B0),
+          [B1] "v"(B1), [B2] "v"(B2), [B3] "v"(B3), [B4] "v"(B4));
+    auto pass = [](float nx, float ny, float nz, float fx, float fy, float fz) -> bool {
+        const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
+        return !(tf - tn < 0.0f) && !(tf < 0.0f);
     };
-    const uint32_t m0 = __ballot(cull(r0.x, a0.x, b0.x) >= 0) != 0ull ? 1u : 0u;
-    const uint32_t m1 = __ballot(cull(r0.y, a0.y, b0.y) >= 0) != 0ull ? 2u : 0u;
-    const uint32_t m2 = __ballot(cull(r1.x, a1.x, b1.x) >= 0) != 0ull ? 4u : 0u;
-    const uint32_t m3 = __ballot(cull(r1.y, a1.y, b1.y) >= 0) != 0ull ? 8u : 0u;
-    return (m0 | m1) | (m2 | m3);
+    const uint32_t m0 = __ballot(pass(nx.x, ny.x, nz.x, ux.x, uy.x, uz.x)) != 0ull ? 1u : 0u;
+    const uint32_t m1 = __ballot(pass(nx.y, ny.y, nz.y, ux.y, uy.y, uz.y)) != 0ull ? 2u : 0u;
+    return m0 | m1;
+}
+__device__ __forceinline__ uint32_t box_mask(const BoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
+    return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
 }
 
 // The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
@@ -515,20 +537,26 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         float oe2 = __builtin_fmaf(foz, e2z, __builtin_fmaf(foy, e2y, fox * e2x));
         // Degenerate lanes: L*af must not underflow (L >= 1e-15: d within ~3e-8 of the y axis), and
         // x^2, y^2 must stay finite (|c|_1 + |o|_1 <= 1e15), so D is never inf - inf.
-        // Behind test of the cluster bounds (cluster_mask): h = d^ sg, and -(o.h) + 16 u pm, the margin
-        // covering the fp32 rounding of C.h - o.h (|C|_1 <= cmax).
-        const float sh = (1.0f / sqrtf(af)) * sg;
-        float hx = fdx * sh, hy = fdy * sh, hz = fdz * sh;
-        float noh = __builtin_fmaf(pm, 16.0f * 0x1.0p-24f, -__builtin_fmaf(foz, hz, __builtin_fmaf(foy, hy, fox * hx)));
+        // Cluster boxes (box_mask): i = 1/d per axis (|d_a| clamped to >= 1e-20, keeping its sign: a
+        // ray parallel to a slab then has near/far times of ~1e20 and the slab test stays exact in
+        // effect), A = -o.i, and J = |i| (1 + kappa).  kappa widens every box by kappa h >= kappa
+        // sqrt(r2min) (h >= sqrt(r2min), pack_sweep): m / (2 sqrt(r2min)) covers the reference's own
+        // rounding (a hit point lies within sqrt(r2f + m) <= sqrt(r2f) + m / (2 sqrt(r2min)) of its
+        // sphere's centre, m as for the sphere filter), 8 u pm the fp32 rounding of u, near and far.
+        auto inv_ax = [](float v) -> float { return 1.0f / (fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v)); };
+        float ix = inv_ax(fdx), iy = inv_ax(fdy), iz = inv_ax(fdz);
+        const float kap = 1.0f + (m * 0.5f + 8.0f * 0x1.0p-24f * pm * sqrtf(qa.f_r2min)) / qa.f_r2min;
+        float Jx = fabsf(ix) * kap, Jy = fabsf(iy) * kap, Jz = fabsf(iz) * kap;
+        float Ax = -(fox * ix), Ay = -(foy * iy), Az = -(foz * iz);
         if (!(L >= 1e-15f) || !(pm <= 1e15f)) {   // zero basis: x = y = 0, every real sphere passes
             e1x = e1z = e2x = e2y = e2z = 0.0f;
             oe1 = oe2 = 0.0f;
-            hx = hy = hz = noh = 0.0f;
+            ix = iy = iz = Jx = Jy = Jz = Ax = Ay = Az = 0.0f;   // box times all 0 (or NaN): every box passes
         }
         // Two per-lane constants per VGPR pair; every use broadcasts one half through the packed
         // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
         const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, 0.0f}, K3 = {-oe1, -oe2};
-        const f2 K4 = {hx, hy}, K5 = {hz, noh};
+        const f2 B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, 0.0f};
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222).
         auto exact4 = [&](uint32_t g) {
             KSTAT(0);
@@ -597,12 +625,12 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // test.  The phases never hold both SGPR pipelines at once (no SGPR spills).
         const uint32_t nxg = qa.n_xg, ntop = qa.n_top;
         for (uint32_t g = 0; g < nxg; ++g) exact4(g);
-        cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 64);
+        cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 32);
         for (uint32_t t0 = 0; t0 < ntop; t0 += 8u) {
             uint32_t mask = 0;
-            sphere_loop(ft + 16u * t0, min(8u, ntop - t0), [&](const SphGroup<float>& cur, uint32_t t) {
+            box_loop(ft + kBoxFloats * t0, min(8u, ntop - t0), [&](const BoxGroup& cur, uint32_t t) {
                 KSTAT(5);
-                mask |= cluster_mask(cur, K0, K1, K2, K3, K4, K5) << (4u * t);
+                mask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
             });
             while (mask != 0u) {
                 const uint32_t g0 = nxg + 4u * (4u * t0 + (uint32_t)__builtin_ctz(mask));
@@ -1633,11 +1661,11 @@ static SweepLayout build_layout(const rt_scene* s) {
 }
 
 // Slot-order streams for rays in precision T: the exact groups (SphGroup layout of pack_scene),
-// the fp32 filter groups (pack_filter's records) and the top stream of cluster bounds, fp32 groups
-// of 4 {cx, cy, cz, R2}: the mean of the members' fp32 centres and R2 >= (max |c_i - C| + r_i)^2
-// (r_i from the member's filter r2f, so the floor applies), inflated by 2^-20 relative and 4 u |.|_1
-// for the fp32 rounding of C; +inf if any member is always exact, -inf for an empty cluster.  The
-// bounds enter the margin maxima (cmax, r2max) like spheres; r2min is unchanged (R2 >= any member r2f).
+// the fp32 filter groups (pack_filter's records) and the top stream of cluster bounds: axis-aligned
+// boxes {centre C, half-extent h} in fp32, 4 per 96-byte group (BoxGroup), enclosing every member
+// with its filter radius sqrt(r2f) (so the floor applies: h >= sqrt(r2min) on every axis), h rounded
+// up and widened by 2^-20 relative and 4 u |C| for the fp32 rounding of C; h = +inf if a member is
+// always exact in T, -inf for an empty cluster.  |C|_1 + |h|_1 enters the margin bound cmax.
 template <typename T>
 static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec, const SweepLayout& L,
                        std::vector<T>& rgrp, std::vector<float>& rfgrp, std::vector<float>& top, float& cmax,
@@ -1669,43 +1697,36 @@ static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec
         }
     }
     const size_t nc = L.members.size();
-    top.assign((size_t)4 * (nc + 4), 0.0f);   // + one empty top group (prefetch target)
-    double cm = cmax, rm = r2max;
+    top.assign((size_t)kBoxFloats / 4 * (nc + 4), 0.0f);   // + one empty top group (prefetch target)
+    double cm = cmax;
     for (size_t k = 0; k < nc + 4; ++k) {
-        float b[4] = {0.0f, 0.0f, 0.0f, -INFINITY};
+        float b[6] = {0.0f, 0.0f, 0.0f, -INFINITY, -INFINITY, -INFINITY};   // empty: never passes
         if (k < nc && !L.members[k].empty()) {
-            const auto& m = L.members[k];
-            double C[3] = {0, 0, 0};
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
             bool inf = false;
-            for (uint32_t i : m) {
-                for (int a = 0; a < 3; ++a) C[a] += (double)frec[4 * i + a];
+            for (uint32_t i : L.members[k]) {
+                const double r = std::sqrt((double)frec[4 * i + 3]);   // the filter's (floored) radius
                 if (!(frec[4 * i + 3] < INFINITY)) inf = true;
-            }
-            for (int a = 0; a < 3; ++a) b[a] = (float)(C[a] / (double)m.size());
-            if (inf) {
-                b[3] = INFINITY;
-            } else {
-                double R = 0.0, r2m = 0.0, c1 = 0.0;
-                for (uint32_t i : m) {
-                    const double dx = frec[4 * i] - (double)b[0], dy = frec[4 * i + 1] - (double)b[1],
-                                 dz = frec[4 * i + 2] - (double)b[2];
-                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::sqrt((double)frec[4 * i + 3]));
-                    r2m = std::max(r2m, (double)frec[4 * i + 3]);
-                    c1 = std::max(c1, std::fabs((double)frec[4 * i]) + std::fabs((double)frec[4 * i + 1]) +
-                                          std::fabs((double)frec[4 * i + 2]));
+                for (int a = 0; a < 3; ++a) {
+                    lo[a] = std::min(lo[a], (double)frec[4 * i + a] - r);
+                    hi[a] = std::max(hi[a], (double)frec[4 * i + a] + r);
                 }
-                const double cb = std::fabs((double)b[0]) + std::fabs((double)b[1]) + std::fabs((double)b[2]);
-                R = R * (1.0 + 0x1.0p-20) + 0x1.0p-22 * (cb + c1);
-                b[3] = up32(std::max(R * R, r2m));
-                cm = std::max(cm, cb);
-                rm = std::max(rm, (double)b[3]);
             }
+            double c1 = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                b[a] = (float)(0.5 * (lo[a] + hi[a]));
+                const double h = std::max(hi[a] - (double)b[a], (double)b[a] - lo[a]);
+                b[3 + a] = inf ? INFINITY : up32(h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a]));
+                c1 += std::fabs((double)b[a]) + (double)b[3 + a];
+            }
+            if (!inf) cm = std::max(cm, c1);
         }
+        // pair-interleaved: pair q of a group at 12 q, {cx0,cx1, cy0,cy1, cz0,cz1, hx0,hx1, hy0,hy1, hz0,hz1}
         const size_t tg = k / 4, j = k % 4;
-        for (int f = 0; f < 4; ++f) top[16 * tg + 8 * (j / 2) + 2 * f + (j % 2)] = b[f];
+        for (int f = 0; f < 6; ++f) top[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
     }
     cmax = up32(cm);
-    r2max = up32(rm);
+    (void)r2max;
 }
 
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
