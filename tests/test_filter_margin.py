@@ -104,3 +104,36 @@ def test_camera_cone_cull_is_conservative(cone_fuzz_bin, f64):
     assert r.returncode == 0 and misses == 0, r.stdout
     assert hits > 1000000 and culled > 50000, r.stdout   # both sides of tangency are exercised
     assert worst < 64.0 / 4, r.stdout
+
+
+@pytest.fixture(scope="module")
+def box_fuzz_bin(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("boxfuzz") / "box_cull_fuzz")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", out, os.path.join(HERE, "box_cull_fuzz.c"), "-lm"],
+                   check=True)
+    return out
+
+
+def test_box_margin_constants_match_kernel():
+    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    fz = open(os.path.join(HERE, "box_cull_fuzz.c")).read()
+    kap = "(m * 0.5f + 8.0f * 0x1.0p-24f * pm * sqrtf(qa.f_r2min)) / qa.f_r2min"
+    assert kap in src and kap.replace("m * 0.5f", "mm * 0.5f").replace("0x1.0p-24f * pm", "u * pm") \
+        .replace("qa.f_r2min", "fr2min") in fz
+    box = "h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a])"
+    assert box in src and "hh * (1.0 + 0x1.0p-20) + 0x1.0p-22 * fabs((double)C[a])" in fz
+    assert "fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v)" in src
+
+
+@pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
+def test_cluster_box_is_conservative(box_fuzz_bin, f64):
+    """General sweep: a cluster whose member the reference hits (Q1, root2 or scalar test) passes
+    the lane's slab test against the cluster box, with a quarter of the margin too (>= 4x headroom)."""
+    r = subprocess.run([box_fuzz_bin, "1500000", str(f64), str(0x9E3779B97F4A7C15 ^ (f64 + 7))], capture_output=True,
+                       text=True, timeout=300)
+    fields = r.stdout.split()
+    hits = int(fields[fields.index("hits") + 1])
+    culled = int(fields[fields.index("culled") + 1])
+    assert r.returncode == 0 and int(fields[fields.index("misses") + 1]) == 0, r.stdout
+    assert int(fields[fields.index("quarter-margin-misses") + 1]) == 0, r.stdout
+    assert hits > 500000 and culled > 200000, r.stdout
