@@ -114,6 +114,7 @@ template <typename T> struct KParams {
     uint32_t n_fgroups;
     float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
     float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
+    float f_ir2, f_hir2, f_isr; // 1/r2min, 0.5/r2min and 8 u/sqrt(r2min), rounded up (launch_t)
     const float* cull;         // camera cone-cull table: {wx, wy, wz, rp} per sphere (build_cam_table)
     const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
     // general sweep, two-level (build_layout / pack_sweep): slot-order exact and filter streams,
@@ -529,8 +530,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         const float m = kFilterMargin * __builtin_fmaf(pm, pm, qa.f_r2max);
         // Basis scaled by sg = 1/sqrt(1 + m/r2min): x'^2 + y'^2 <= r2f is x^2 + y^2 <= r2f (1 + m/r2min)
         // >= r2f + m for every sphere (r2f >= r2min), so the margin needs no per-pair add.
-        const float sg = 1.0f / sqrtf(1.0f + m / qa.f_r2min);
-        const float s1 = (1.0f / sqrtf(L)) * sg, s2 = (1.0f / sqrtf(L * af)) * sg;
+        // The filter constants need no correctly rounded division or square root: v_rsq_f32 and
+        // v_rcp_f32 (1 ulp) add a few u to the basis error, well inside the margin (the fuzz tests
+        // model them as +-1 ulp).  1/r2min, 0.5/r2min and 8u/sqrt(r2min) come from the host.
+        const float sg = __builtin_amdgcn_rsqf(__builtin_fmaf(m, qa.f_ir2, 1.0f));
+        const float s1 = __builtin_amdgcn_rsqf(L) * sg, s2 = __builtin_amdgcn_rsqf(L * af) * sg;
         float e1x = fdz * s1, e1z = -fdx * s1;
         float e2x = -(fdx * fdy) * s2, e2y = L * s2, e2z = -(fdy * fdz) * s2;
         float oe1 = __builtin_fmaf(foz, e1z, fox * e1x);
@@ -543,9 +547,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // sqrt(r2min) (h >= sqrt(r2min), pack_sweep): m / (2 sqrt(r2min)) covers the reference's own
         // rounding (a hit point lies within sqrt(r2f + m) <= sqrt(r2f) + m / (2 sqrt(r2min)) of its
         // sphere's centre, m as for the sphere filter), 8 u pm the fp32 rounding of u, near and far.
-        auto inv_ax = [](float v) -> float { return 1.0f / (fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v)); };
+        auto inv_ax = [](float v) -> float {
+            return __builtin_amdgcn_rcpf(fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v));
+        };
         float ix = inv_ax(fdx), iy = inv_ax(fdy), iz = inv_ax(fdz);
-        const float kap = 1.0f + (m * 0.5f + 8.0f * 0x1.0p-24f * pm * sqrtf(qa.f_r2min)) / qa.f_r2min;
+        const float kap = 1.0f + __builtin_fmaf(m, qa.f_hir2, pm * qa.f_isr);   // m / (2 r2min) + 8 u pm / sqrt(r2min)
         float Jx = fabsf(ix) * kap, Jy = fabsf(iy) * kap, Jz = fabsf(iz) * kap;
         float Ax = -(fox * ix), Ay = -(foy * iy), Az = -(foz * iz);
         if (!(L >= 1e-15f) || !(pm <= 1e15f)) {   // zero basis: x = y = 0, every real sphere passes
@@ -1239,6 +1245,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         T bt = T(0);
         int bi = -1;
 #ifndef RT_EXP_NO_CAMCULL
+#ifdef RT_EXP_DUP_CAM   // timing experiment: the camera sweep twice (same result)
+        {
+            V3<T> bd2 = bd;
+            asm volatile("" : "+v"(bd2.x));
+            T bt2;
+            const int bi2 = camera_sweep<T, ROOT2, SC>(v, bd2, bt2);
+            asm volatile("" ::"v"(bi2), "v"(bt2));
+        }
+#endif
         bi = camera_sweep<T, ROOT2, SC>(v, bd, bt);   // whole wave: lanes are spheres in the cull
 #else
         if (v) bi = nearest_hit<T, ROOT2, SC, true>(p, bd, bd, bt);
@@ -1304,6 +1319,14 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (fresh) { sid = nsid; slot = nslot; pix = npix; }
         }
         // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
+#ifdef RT_EXP_DUP_SCATTER   // timing experiment: the next-ray stage twice (same result)
+        if (fresh || scat) {
+            V3<T> o2 = o, d2 = d, c2 = c;
+            asm volatile("" : "+v"(o2.x), "+v"(d2.x), "+v"(c2.x));
+            next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o2, d2, c2);
+            asm volatile("" ::"v"(o2.x), "v"(o2.y), "v"(o2.z), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(c2.x), "v"(c2.y), "v"(c2.z));
+        }
+#endif
         if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
         if (fresh) {
             k = 0;
@@ -1317,6 +1340,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const uint32_t depth = cold_args<T>()->depth;
         const bool act = live && k < depth;
         hit_i = -1;
+#ifdef RT_EXP_DUP_SWEEP   // timing experiment: the general sweep twice (same result)
+        if (act) {
+            V3<T> o2 = o;
+            asm volatile("" : "+v"(o2.x));
+            T t2;
+            const int h2 = nearest_hit<T, ROOT2, SC>(p, o2, d, t2);
+            asm volatile("" ::"v"(h2), "v"(t2));
+        }
+#endif
         if (act) hit_i = nearest_hit<T, ROOT2, SC>(p, o, d, hit_t);
         const unsigned long long bact = __ballot(act);
         if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
@@ -1841,6 +1873,17 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
     p.f_r2min = f64 ? c->f_r2min64 : c->f_r2min32;
+    {
+        auto up32 = [](double v) -> float {
+            float f = (float)v;
+            if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+            return f;
+        };
+        const double r2m = (double)p.f_r2min;   // 0 (no filtered sphere) gives +inf: every basis is zero
+        p.f_ir2 = up32(1.0 / r2m);
+        p.f_hir2 = up32(0.5 / r2m);
+        p.f_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m));
+    }
     bool filter_off = false;
     {   // diagnostics: every general-sweep and camera-sweep group through the exact test
         const char* e = getenv("RT_FILTER_OFF");

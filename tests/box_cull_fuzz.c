@@ -17,6 +17,13 @@ static uint64_t s = 88172645463325252ull;
 static double U() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (s >> 11) * 0x1.0p-53; }
 static double N() { double a = U(), b = U(); return sqrt(-2 * log(a + 1e-300)) * cos(6.283185307179586 * b); }
 static float up32(double v) { float f = (float)v; if ((double)f < v) f = nextafterf(f, INFINITY); return f; }
+// v_rcp_f32 (1 ulp): the correctly rounded value moved by -1, 0 or +1 ulp at random
+static float rcp(float x) {
+    float r = 1.0f / x;
+    const double v = U();
+    if (v < 1.0 / 3) r = nextafterf(r, 0.0f); else if (v < 2.0 / 3) r = nextafterf(r, copysignf(INFINITY, r));
+    return r;
+}
 
 static int hits_f(const float o[3], const float d[3], const float c[3], float r) {
     const float oc[3] = {o[0] - c[0], o[1] - c[1], o[2] - c[2]}, r2 = r * r;
@@ -157,11 +164,11 @@ int main(int argc, char** argv) {
         const float on = fabsf(fo[0]) + fabsf(fo[1]) + fabsf(fo[2]);
         const float pm = cmax + on;
         const float mm = 48.0f * 0x1.0p-24f * fmaf(pm, pm, fr2max);
-        const float kap = 1.0f + (mm * 0.5f + 8.0f * u * pm * sqrtf(fr2min)) / fr2min;
+        const float kap = 1.0f + fmaf(mm, up32(0.5 / fr2min), pm * up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min)));
         const float kq = 1.0f + (kap - 1.0f) * 0.25f;
         float I[3], A[3], J[3], Jq[3], J0[3];
         for (int a = 0; a < 3; ++a) {
-            I[a] = 1.0f / (fabsf(fd[a]) >= 1e-20f ? fd[a] : copysignf(1e-20f, fd[a]));
+            I[a] = rcp(fabsf(fd[a]) >= 1e-20f ? fd[a] : copysignf(1e-20f, fd[a]));
             A[a] = -(fo[a] * I[a]);
             J[a] = fabsf(I[a]) * kap;
             Jq[a] = fabsf(I[a]) * kq;

@@ -19,6 +19,14 @@ static uint64_t s = 88172645463325252ull;
 static double U() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (s >> 11) * 0x1.0p-53; }
 static double N() { double a = U(), b = U(); return sqrt(-2 * log(a + 1e-300)) * cos(6.283185307179586 * b); }
 static const float KM = 48.0f * 0x1.0p-24f;
+// v_rsq_f32 (1 ulp): the correctly rounded value moved by -1, 0 or +1 ulp at random
+static float rsq(float x) {
+    float r = 1.0f / sqrtf(x);
+    const double v = U();
+    if (v < 1.0 / 3) r = nextafterf(r, 0.0f); else if (v < 2.0 / 3) r = nextafterf(r, INFINITY);
+    return r;
+}
+static float up32(double v) { float f = (float)v; if ((double)f < v) f = nextafterf(f, INFINITY); return f; }
 int main(int argc, char** argv) {
     const long n = argc > 1 ? atol(argv[1]) : 10000000;
     const int mode = argc > 2 ? atoi(argv[2]) : 0;
@@ -86,7 +94,7 @@ int main(int argc, char** argv) {
         float cx = C[0], cy = C[1], cz = C[2];
         float L = fmaf(fdz, fdz, fdx * fdx);
         float af = fmaf(fdz, fdz, fmaf(fdy, fdy, fdx * fdx));
-        float s1 = 1.0f / sqrtf(L), s2 = 1.0f / sqrtf(L * af);
+        float s1 = rsq(L), s2 = rsq(L * af);
         float on = fabsf(fox) + fabsf(foy) + fabsf(foz);
         // the kernel's m uses the scene-wide max |c|_1 and max r2f, and its r2min is the scene's
         // smallest r2f; this sphere's own values bound those from the unfavourable side, so the
@@ -97,7 +105,7 @@ int main(int argc, char** argv) {
         float r2min = r2f;
         // basis scaled by sigma = 1/sqrt(1 + m/r2min): the test x'^2 + y'^2 <= r2f is
         // x^2 + y^2 <= r2f (1 + m/r2min) >= r2f + m, with no per-pair add
-        float sg = 1.0f / sqrtf(1.0f + m / r2min);
+        float sg = rsq(fmaf(m, up32(1.0 / r2min), 1.0f));
         float t1 = s1 * sg, t2 = s2 * sg;
         float e1x = fdz * t1, e1z = -fdx * t1;
         float e2x = -(fdx * fdy) * t2, e2y = L * t2, e2z = -(fdy * fdz) * t2;

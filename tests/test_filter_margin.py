@@ -117,12 +117,12 @@ def box_fuzz_bin(tmp_path_factory):
 def test_box_margin_constants_match_kernel():
     src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
     fz = open(os.path.join(HERE, "box_cull_fuzz.c")).read()
-    kap = "(m * 0.5f + 8.0f * 0x1.0p-24f * pm * sqrtf(qa.f_r2min)) / qa.f_r2min"
-    assert kap in src and kap.replace("m * 0.5f", "mm * 0.5f").replace("0x1.0p-24f * pm", "u * pm") \
-        .replace("qa.f_r2min", "fr2min") in fz
+    assert "1.0f + __builtin_fmaf(m, qa.f_hir2, pm * qa.f_isr)" in src
+    assert "p.f_hir2 = up32(0.5 / r2m)" in src and "p.f_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m))" in src
+    assert "1.0f + fmaf(mm, up32(0.5 / fr2min), pm * up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min)))" in fz
     box = "h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a])"
     assert box in src and "hh * (1.0 + 0x1.0p-20) + 0x1.0p-22 * fabs((double)C[a])" in fz
-    assert "fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v)" in src
+    assert "__builtin_amdgcn_rcpf(fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v))" in src
 
 
 @pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
