@@ -115,7 +115,8 @@ template <typename T> struct KParams {
     float f_cmax, f_r2max;     // filter margin bounds: max |c|_1 and max r2f over non-exact spheres
     float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
     float f_ir2, f_hir2, f_isr; // 1/r2min, 0.5/r2min and 8 u/sqrt(r2min), rounded up (launch_t)
-    const float* cull;         // camera cone-cull table: {wx, wy, wz, rp} per sphere (build_cam_table)
+    const float* cull;         // camera cone-cull records {wx, wy, wz, rp} per slot of the sweep layout
+    const float* cullc;        // ... and per cluster (build_cam_table)
     const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
     // general sweep, two-level (build_layout / pack_sweep): slot-order exact and filter streams,
     // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), slot -> scene index; n_top top groups,
@@ -668,6 +669,10 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 // camera-origin table, bit-identical to the per-ray values) for the passing spheres only, in scene
 // order, so ties and the nearest hit are the reference's.  A batch whose rays spread over more than
 // ~30 degrees (tiny images) skips the cull and tests every sphere exactly.
+// Two levels over the sweep layout (build_layout): the always-exact spheres lane by lane, then the
+// clusters lane by lane against cluster records whose rp bounds every member's (the cone distance is
+// 1-Lipschitz in the centre, and rp_k >= rp_i + |c_i - C| for every member, build_cam_table), then
+// the members of the passing clusters.
 __device__ __forceinline__ float ufl(float x) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(x))); }
 
 template <typename T, bool root2, bool SCALAR>
@@ -679,7 +684,9 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     float ax = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdx), l0));
     float ay = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdy), l0));
     float az = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdz), l0));
-    const float ia = 1.0f / sqrtf(__builtin_fmaf(az, az, __builtin_fmaf(ay, ay, ax * ax)));
+    // v_rsq / v_rcp (1 ulp) below: the cone's sin is inflated by 4 u relative + 8 u, and a's length
+    // error scales t and p alike (covered by rp's 32 u |w|)
+    const float ia = __builtin_amdgcn_rsqf(__builtin_fmaf(az, az, __builtin_fmaf(ay, ay, ax * ax)));
     // wave-uniform: keep the axis and the cone's (cos, sin) in SGPRs
     ax = ufl(ax * ia);
     ay = ufl(ay * ia);
@@ -688,7 +695,7 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const float cx = __builtin_fmaf(fdy, az, -(fdz * ay)), cy = __builtin_fmaf(fdz, ax, -(fdx * az)),
                 cz = __builtin_fmaf(fdx, ay, -(fdy * ax));
     const float dn2 = __builtin_fmaf(fdz, fdz, __builtin_fmaf(fdy, fdy, fdx * fdx));
-    const float s2 = v ? __builtin_fmaf(cz, cz, __builtin_fmaf(cy, cy, cx * cx)) / dn2 : 0.0f;
+    const float s2 = v ? __builtin_fmaf(cz, cz, __builtin_fmaf(cy, cy, cx * cx)) * __builtin_amdgcn_rcpf(dn2) * (1.0f + 0x1.0p-22f) : 0.0f;
     const float dt = __builtin_fmaf(fdz, az, __builtin_fmaf(fdy, ay, fdx * ax));
     bool all = __ballot(v && !(dt > 0.5f)) != 0ull;   // some ray > 60 deg off the axis (or NaN)
     uint32_t sm = __float_as_uint(s2);   // non-negative floats (and NaN above +inf) order as integers
@@ -699,42 +706,71 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     if (!(S < 0.5f)) all = true;
     const float Cc = ufl(sqrtf(__builtin_fmaf(-S, S, 1.0f)));
     const auto& q = *cold_args<T>();
-    const float4* cull = (const float4*)__builtin_assume_aligned(q.cull, 16);
+    const float4* cs = (const float4*)__builtin_assume_aligned(q.cull, 16);    // per slot (sweep layout)
+    const float4* cc = (const float4*)__builtin_assume_aligned(q.cullc, 16);   // per cluster
     cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
-    const uint32_t n = q.n_spheres;
+    cptr<uint32_t> ri = (cptr<uint32_t>)q.ridx;
+    const uint32_t nx = 4u * q.n_xg, ncl = 4u * q.n_top;
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
     T best_t = T(INFINITY);
     int best = -1;
     constexpr bool kBothRoots = root2 || SCALAR;
     KSTAT(3);
-    float4 w = cull[lane];   // the table is padded with a whole dummy block: the prefetch stays in bounds
-    for (uint32_t base = 0; base < n; base += 64u) {
-        const float4 wc = w;
-        w = cull[base + 64u + lane];
+    // cone test of a record {w = c - O, rp}; padding records (rp = -inf) never pass
+    auto cone = [&](const float4& wc) -> bool {
         const float t = __builtin_fmaf(wc.z, az, __builtin_fmaf(wc.y, ay, wc.x * ax));
         const float px = __builtin_fmaf(wc.y, az, -(wc.z * ay)), py = __builtin_fmaf(wc.z, ax, -(wc.x * az)),
                     pz = __builtin_fmaf(wc.x, ay, -(wc.y * ax));
         const float pp = sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
         const float f = __builtin_fmaf(pp, Cc, -(t * S));
-        const bool pass = all ? base + lane < n : !(f > wc.w);   // NaN passes
-        unsigned long long m = __ballot(pass);
+        return wc.w > -INFINITY && (all || !(f > wc.w));   // NaN f passes
+    };
+    // the reference's exact test (objects.rs:252-257 on the camera-origin table) for scene index i
+    auto exact = [&](uint32_t i) {
+        KSTAT(2);
+        const T ocx = cxt[4 * i], ocy = cxt[4 * i + 1], ocz = cxt[4 * i + 2], c = cxt[4 * i + 3];
+        if (v) {
+            T hb, disc;
+            if constexpr (SCALAR) {   // objects.rs:217-222
+                hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
+                disc = hb * hb - a * c;
+            } else {                  // objects.rs:255, 257
+                hb = fma(ocz, d.z, fma(ocy, d.y, ocx * d.x));
+                disc = fma(hb, hb, (-a) * c);
+            }
+            if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
+                hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
+        }
+    };
+    // 1. the always-exact spheres (build_layout's leading slots), lanes as spheres
+    for (uint32_t base = 0; base < nx; base += 64u) {
+        unsigned long long m = __ballot(base + lane < nx && cone(cs[base + lane]));
         while (m != 0ull) {
-            const uint32_t i = base + (uint32_t)__builtin_ctzll(m);
+            const uint32_t s = base + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            KSTAT(2);
-            const T ocx = cxt[4 * i], ocy = cxt[4 * i + 1], ocz = cxt[4 * i + 2], c = cxt[4 * i + 3];
-            if (v) {
-                T hb, disc;
-                if constexpr (SCALAR) {   // objects.rs:217-222
-                    hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
-                    disc = hb * hb - a * c;
-                } else {                  // objects.rs:255, 257
-                    hb = fma(ocz, d.z, fma(ocy, d.y, ocx * d.x));
-                    disc = fma(hb, hb, (-a) * c);
-                }
-                if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
-                    hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
+            exact(ri[s]);
+        }
+    }
+    // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
+    // to 4 passing clusters per pass, 16 lanes each
+    for (uint32_t cb = 0; cb < ncl; cb += 64u) {
+        unsigned long long M = __ballot(cone(cc[cb + lane]));   // the table is padded to whole 64s
+        while (M != 0ull) {
+            uint32_t k[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // empty quarters take the padding cluster ncl (all dummies)
+                k[j] = M != 0ull ? cb + (uint32_t)__builtin_ctzll(M) : ncl;
+                M &= M - 1ull;
+            }
+            const uint32_t qd = lane >> 4;
+            const uint32_t kl = qd == 0 ? k[0] : qd == 1 ? k[1] : qd == 2 ? k[2] : k[3];
+            unsigned long long m = __ballot(cone(cs[nx + 16u * kl + (lane & 15u)]));
+            while (m != 0ull) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                const uint32_t kb = (b >> 4) == 0 ? k[0] : (b >> 4) == 1 ? k[1] : (b >> 4) == 2 ? k[2] : k[3];
+                exact(ri[nx + 16u * kb + (b & 15u)]);
             }
         }
     }
@@ -844,9 +880,11 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
 // Also the camera filter table (fp32, groups of 4 spheres), used by the camera-batch sweep under Q1.
 template <typename T, bool SCALAR>
 __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* camf, uint32_t n_fslots, T ox, T oy,
-                                T oz, uint32_t pass_all, T* camx, float* cull, uint32_t n_cull, uint32_t n_real) {
+                                T oz, uint32_t pass_all, T* camx, float* cull, uint32_t n_cull, uint32_t n_real,
+                                const uint32_t* ridx, uint32_t n_cslots, const double* clus, float* cullc,
+                                uint32_t n_clp) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_slots && i >= n_fslots && i >= n_cull) return;
+    if (i >= n_slots && i >= n_fslots && i >= n_cull && i >= n_cslots && i >= n_clp) return;
     constexpr uint32_t G = kGroup<T>, NE = 64 / sizeof(T);
     const uint32_t g = i / G, j = i % G;
     auto at = [&](uint32_t f) -> uint32_t {
@@ -878,25 +916,50 @@ __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* c
         float* out = camf + 16 * fg + 8 * (fj / 2) + (fj % 2);
         out[0] = (float)ocx; out[2] = (float)ocy; out[4] = (float)ocz; out[6] = sc;
     }
-    if (i < n_cull) {
-        // Per-sphere AoS copy of the camera-origin record, and the cone-cull record (camera_sweep):
-        // w = c - O in fp32 and rp = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w| rounded up (u = 2^-24);
-        // +inf (always tested) for non-finite values and under RT_FILTER_OFF, -inf for the padding.
+    if (i < n_cull) {   // per-sphere (scene index) AoS copy of the camera-origin record
         T ex = T(0), ey = T(0), ez = T(0), ec = T(INFINITY);
-        float rp = -INFINITY;
-        if (i < n_real) {
-            ex = ocx; ey = ocy; ez = ocz; ec = c;
-            const double wx = (double)ocx, wy = (double)ocy, wz = (double)ocz;
-            const double wn2 = wx * wx + wy * wy + wz * wz, r2 = (double)sph[at(3)];
-            const double v = sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30;
-            rp = INFINITY;
-            if (!pass_all && v < 1e30) {
-                rp = (float)v;
-                if ((double)rp < v) rp = nextafterf(rp, INFINITY);
-            }
-        }
+        if (i < n_real) { ex = ocx; ey = ocy; ez = ocz; ec = c; }
         camx[4 * i] = ex; camx[4 * i + 1] = ey; camx[4 * i + 2] = ez; camx[4 * i + 3] = ec;
-        cull[4 * i] = -(float)ex; cull[4 * i + 1] = -(float)ey; cull[4 * i + 2] = -(float)ez; cull[4 * i + 3] = rp;
+    }
+    auto rup = [](double v) -> float {   // fp32 >= v; +inf past 1e30 (and for NaN)
+        if (!(v < 1e30)) return INFINITY;
+        float f = (float)v;
+        if ((double)f < v) f = nextafterf(f, INFINITY);
+        return f;
+    };
+    if (i < n_cslots) {
+        // Cone-cull record of slot i of the sweep layout (camera_sweep): w = c - O in fp32 and
+        // rp = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w| rounded up (u = 2^-24); +inf (always tested)
+        // for non-finite values and under RT_FILTER_OFF, -inf for dummy slots (never pass).
+        const uint32_t sj = ridx[i];
+        float w[3] = {0.0f, 0.0f, 0.0f}, rp = -INFINITY;
+        if (sj != 0xFFFFFFFFu) {
+            const uint32_t gj = sj / G, jj = sj % G;
+            auto atj = [&](uint32_t f) -> uint32_t {
+                return sizeof(T) == 4 ? gj * NE + 8 * (jj / 2) + 2 * f + (jj % 2) : gj * NE + 4 * jj + f;
+            };
+            const T wx = sph[atj(0)] - ox, wy = sph[atj(1)] - oy, wz = sph[atj(2)] - oz;   // = -(o - c) exactly
+            const double wn2 = (double)wx * (double)wx + (double)wy * (double)wy + (double)wz * (double)wz;
+            const double r2 = (double)sph[atj(3)];
+            rp = pass_all ? INFINITY : rup(sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30);
+            w[0] = (float)wx; w[1] = (float)wy; w[2] = (float)wz;
+        }
+        cull[4 * i] = w[0]; cull[4 * i + 1] = w[1]; cull[4 * i + 2] = w[2]; cull[4 * i + 3] = rp;
+    }
+    if (i < n_clp) {
+        // Cluster record: W = C - O and rp_k = R (1 + 2^-20) + (2^-9 + 2^-16) (|W| + R) (C, R: the
+        // cluster's bounding sphere, set_scene; R = -inf: padding, never passes).  A member's rp_i <=
+        // r_i (1 + 2^-21) + (2^-9 + 2^-19) |w_i| (sqrt(64 u) = 2^-9) and |w_i| <= |W| + R, so rp_k >=
+        // rp_i + |c_i - C| plus the fp32 evaluation errors of both records (camera_sweep).
+        const double R = clus[4 * i + 3];
+        float w[3] = {0.0f, 0.0f, 0.0f}, rp = -INFINITY;
+        if (R > -INFINITY) {
+            const double wx = clus[4 * i] - (double)ox, wy = clus[4 * i + 1] - (double)oy, wz = clus[4 * i + 2] - (double)oz;
+            const double wn = sqrt(wx * wx + wy * wy + wz * wz);
+            rp = pass_all ? INFINITY : rup(R * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (wn + R) + 1e-30);
+            w[0] = (float)wx; w[1] = (float)wy; w[2] = (float)wz;
+        }
+        cullc[4 * i] = w[0]; cullc[4 * i + 1] = w[1]; cullc[4 * i + 2] = w[2]; cullc[4 * i + 3] = rp;
     }
 }
 
@@ -1410,6 +1473,9 @@ struct rt_context {
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
     uint32_t* ridx = nullptr;
+    void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
+    void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
+    uint32_t n_cslots = 0, n_clp = 0;                 // slot-order cull records; cluster records (x64)
     uint32_t n_top = 0, n_xg = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
@@ -1497,6 +1563,9 @@ static void free_scene(rt_context* c) {
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
     (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
+    (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
+    c->clus64 = c->clus32 = c->cullc64 = c->cullc32 = nullptr;
+    c->n_cslots = c->n_clp = 0;
     c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
     c->ridx = nullptr;
     c->n_top = c->n_xg = 0;
@@ -1799,10 +1868,48 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32;
         pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64);
         pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32);
-        std::vector<uint32_t> ridx(L.slot.size() + 4, 0u);
-        for (size_t i = 0; i < L.slot.size(); ++i) ridx[i] = L.slot[i] < 0 ? 0u : (uint32_t)L.slot[i];
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
+        // slot -> scene index (0xFFFFFFFF: dummy), padded past the last cluster by one block of 64
+        // (the camera sweep's empty quarters read the slots of cluster index n_clusters)
+        const uint32_t ncl = (uint32_t)L.members.size();
+        c->n_cslots = 4u * L.n_xg + 16u * ncl + 64u;
+        c->n_clp = (ncl + 63u) / 64u * 64u;
+        std::vector<uint32_t> ridx(c->n_cslots, 0xFFFFFFFFu);
+        for (size_t i = 0; i < L.slot.size(); ++i) if (L.slot[i] >= 0) ridx[i] = (uint32_t)L.slot[i];
+        // cluster bounding spheres for the camera cull, per precision: centre = the members' AABB
+        // centre, R >= max |c_i - C| + |r_i| over the members' T-precision centres and radii
+        auto bounds = [&](auto const& cen, std::vector<double>& out) {
+            out.assign((size_t)4 * (c->n_clp ? c->n_clp : 1), 0.0);
+            for (size_t k = 0; k < out.size() / 4; ++k) out[4 * k + 3] = -INFINITY;
+            for (uint32_t k = 0; k < ncl; ++k) {
+                const auto& m = L.members[k];
+                if (m.empty()) continue;
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                for (uint32_t i : m)
+                    for (int a = 0; a < 3; ++a) {
+                        const double r = std::fabs((double)cen[4 * i + 3]);
+                        lo[a] = std::min(lo[a], (double)cen[4 * i + a] - r);
+                        hi[a] = std::max(hi[a], (double)cen[4 * i + a] + r);
+                    }
+                double C[3], R = 0.0;
+                for (int a = 0; a < 3; ++a) C[a] = 0.5 * (lo[a] + hi[a]);
+                for (uint32_t i : m) {
+                    const double dx = (double)cen[4 * i] - C[0], dy = (double)cen[4 * i + 1] - C[1],
+                                 dz = (double)cen[4 * i + 2] - C[2];
+                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs((double)cen[4 * i + 3]));
+                }
+                out[4 * k] = C[0]; out[4 * k + 1] = C[1]; out[4 * k + 2] = C[2];
+                out[4 * k + 3] = std::isfinite(R) ? R * (1.0 + 0x1.0p-40) : INFINITY;
+            }
+        };
+        std::vector<double> cl64, cl32;
+        bounds(c64, cl64);
+        bounds(c32, cl32);
+        if ((rc = up(&c->clus64, cl64.data(), cl64.size() * sizeof(double))) != RT_OK) return rc;
+        if ((rc = up(&c->clus32, cl32.data(), cl32.size() * sizeof(double))) != RT_OK) return rc;
+        HIPCHK(hipMalloc(&c->cullc64, cl64.size() / 4 * 4 * sizeof(float)));
+        HIPCHK(hipMalloc(&c->cullc32, cl32.size() / 4 * 4 * sizeof(float)));
         if ((rc = up(&c->rsph64, rg64.data(), rg64.size() * sizeof(double))) != RT_OK) return rc;
         if ((rc = up(&c->rsph32, rg32.data(), rg32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->rfsph64, rf64.data(), rf64.size() * sizeof(float))) != RT_OK) return rc;
@@ -1818,8 +1925,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     c->n_cull = (s->n_spheres + 63u) / 64u * 64u + 64u;
     HIPCHK(hipMalloc(&c->camx64, (size_t)4 * c->n_cull * sizeof(double)));
     HIPCHK(hipMalloc(&c->camx32, (size_t)4 * c->n_cull * sizeof(float)));
-    HIPCHK(hipMalloc(&c->cull64, (size_t)4 * c->n_cull * sizeof(float)));
-    HIPCHK(hipMalloc(&c->cull32, (size_t)4 * c->n_cull * sizeof(float)));
+    HIPCHK(hipMalloc(&c->cull64, (size_t)4 * c->n_cslots * sizeof(float)));
+    HIPCHK(hipMalloc(&c->cull32, (size_t)4 * c->n_cslots * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->cen32, c32.data(), c32.size() * sizeof(float))) != RT_OK) return rc;
     if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
@@ -1934,11 +2041,13 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         p.camx = (const T*)(f64 ? c->camx64 : c->camx32);
         p.cull = (const float*)(f64 ? c->cull64 : c->cull32);
         const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>, n_fslots = (p.n_fgroups + 1) * 4;
-        const uint32_t n_thr = std::max(std::max(n_slots, n_fslots), c->n_cull);
+        p.cullc = (const float*)(f64 ? c->cullc64 : c->cullc32);
+        const uint32_t n_thr = std::max(std::max(std::max(n_slots, n_fslots), c->n_cull), std::max(c->n_cslots, c->n_clp));
         auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
         hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
                            (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off,
-                           (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres);
+                           (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres, c->ridx, c->n_cslots,
+                           (const double*)(f64 ? c->clus64 : c->clus32), (float*)p.cullc, c->n_clp);
         HIPCHK(hipGetLastError());
     }
     int per_cu = 0;

@@ -7,7 +7,7 @@
 // !(f > rp) with rp = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w| rounded up.
 // Cases: batches of 1..64 rays with angular spreads 1e-7..0.3 rad, spheres placed near tangency to
 // one ray of the batch, cameras near and inside spheres, scales 0.1..1000, fp32 and fp64 rays.
-// Prints the worst k with f <= sqrt(r^2 + k u |w|^2) over all hits (the kernel's k is 64).
+// Prints the worst fraction of the margin used over all hits: (f - r) / (rp - r).
 // Usage: cone_cull_fuzz N F64(0|1) [SEED]
 #include <math.h>
 #include <stdint.h>
@@ -19,6 +19,13 @@ static double U() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (s >> 11) * 
 static double N() { double a = U(), b = U(); return sqrt(-2 * log(a + 1e-300)) * cos(6.283185307179586 * b); }
 static float up32(double v) { float f = (float)v; if ((double)f < v) f = nextafterf(f, INFINITY); return f; }
 static uint32_t bits(float x) { uint32_t b; memcpy(&b, &x, 4); return b; }
+// v_rsq_f32 / v_rcp_f32 (1 ulp): the correctly rounded value moved by -1, 0 or +1 ulp at random
+static float jitter(float r) {
+    const double v = U();
+    return v < 1.0 / 3 ? nextafterf(r, 0.0f) : v < 2.0 / 3 ? nextafterf(r, INFINITY) : r;
+}
+static float rsq(float x) { return jitter(1.0f / sqrtf(x)); }
+static float rcp(float x) { return jitter(1.0f / x); }
 static float fbits(uint32_t b) { float x; memcpy(&x, &b, 4); return x; }
 
 // Does any of the three reference tests find a valid root?  (T = float)
@@ -63,8 +70,7 @@ int main(int argc, char** argv) {
     long n = atol(argv[1]);
     int f64 = atoi(argv[2]);
     if (argc > 3) s = strtoull(argv[3], 0, 0) | 1;
-    const double u = 0x1.0p-24;
-    long hits = 0, miss = 0, culled = 0, batches_all = 0;
+    long hits = 0, miss = 0, culled = 0, batches_all = 0, cmiss = 0;
     double worst = -1e300;
     for (long it = 0; it < n; ++it) {
         const double S = pow(10.0, -1 + 4 * U());
@@ -124,7 +130,7 @@ int main(int argc, char** argv) {
         const float rp = v < 1e30 ? up32(v) : INFINITY;
         // camera_sweep: the cone, as the kernel computes it
         float ax = Df[0][0], ay = Df[0][1], az = Df[0][2];
-        const float ia = 1.0f / sqrtf(fmaf(az, az, fmaf(ay, ay, ax * ax)));
+        const float ia = rsq(fmaf(az, az, fmaf(ay, ay, ax * ax)));
         ax = ax * ia; ay = ay * ia; az = az * ia;
         uint32_t sm = 0;
         int all = 0;
@@ -132,7 +138,7 @@ int main(int argc, char** argv) {
             const float fdx = Df[i][0], fdy = Df[i][1], fdz = Df[i][2];
             const float cx = fmaf(fdy, az, -(fdz * ay)), cy = fmaf(fdz, ax, -(fdx * az)), cz = fmaf(fdx, ay, -(fdy * ax));
             const float dn2 = fmaf(fdz, fdz, fmaf(fdy, fdy, fdx * fdx));
-            const float s2 = fmaf(cz, cz, fmaf(cy, cy, cx * cx)) / dn2;
+            const float s2 = fmaf(cz, cz, fmaf(cy, cy, cx * cx)) * rcp(dn2) * (1.0f + 0x1.0p-22f);
             const float dt = fmaf(fdz, az, fmaf(fdy, ay, fdx * ax));
             if (!(dt > 0.5f)) all = 1;
             if (bits(s2) > sm) sm = bits(s2);
@@ -145,19 +151,51 @@ int main(int argc, char** argv) {
         const float pp = sqrtf(fmaf(qz, qz, fmaf(qy, qy, qx * qx)));
         const float f = fmaf(pp, Cc, -(t * Sn));
         const int pass = all || !(f > rp);
+        // the sphere's cluster (set_scene's bounds + build_cam_table's record): the target plus up to
+        // 15 neighbours; AABB centre C, R >= max |c_i - C| + r_i, rp_k as the kernel computes it
+        double cl[16][4];
+        const int nk = 1 + (int)(U() * 16);
+        for (int k = 0; k < 3; ++k) cl[0][k] = f64 ? C[k] : (double)(float)C[k];
+        cl[0][3] = f64 ? r : (double)(float)r;
+        for (int m = 1; m < nk; ++m) {
+            for (int k = 0; k < 3; ++k) cl[m][k] = C[k] + N() * S * 0.05;
+            cl[m][3] = r * pow(10.0, 2 * U() - 1);
+            if (!f64) for (int k = 0; k < 4; ++k) cl[m][k] = (float)cl[m][k];
+        }
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY}, CC[3], RR = 0.0;
+        for (int m = 0; m < nk; ++m)
+            for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], cl[m][k] - cl[m][3]); hi[k] = fmax(hi[k], cl[m][k] + cl[m][3]); }
+        for (int k = 0; k < 3; ++k) CC[k] = 0.5 * (lo[k] + hi[k]);
+        for (int m = 0; m < nk; ++m) {
+            const double dx = cl[m][0] - CC[0], dy = cl[m][1] - CC[1], dz = cl[m][2] - CC[2];
+            RR = fmax(RR, sqrt(dx * dx + dy * dy + dz * dz) + cl[m][3]);
+        }
+        RR *= 1.0 + 0x1.0p-40;
+        const double Ox = f64 ? O[0] : (double)(float)O[0], Oy = f64 ? O[1] : (double)(float)O[1],
+                     Oz = f64 ? O[2] : (double)(float)O[2];
+        const double Wx = CC[0] - Ox, Wy = CC[1] - Oy, Wz = CC[2] - Oz, Wn = sqrt(Wx * Wx + Wy * Wy + Wz * Wz);
+        const double vk = RR * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (Wn + RR) + 1e-30;
+        const float rpk = vk < 1e30 ? up32(vk) : INFINITY;
+        const float Wf[3] = {(float)Wx, (float)Wy, (float)Wz};
+        const float tk = fmaf(Wf[2], az, fmaf(Wf[1], ay, Wf[0] * ax));
+        const float kx = fmaf(Wf[1], az, -(Wf[2] * ay)), ky = fmaf(Wf[2], ax, -(Wf[0] * az)), kz = fmaf(Wf[0], ay, -(Wf[1] * ax));
+        const float pk = sqrtf(fmaf(kz, kz, fmaf(ky, ky, kx * kx)));
+        const int pass_k = all || !(fmaf(pk, Cc, -(tk * Sn)) > rpk);
+        if (pass && !pass_k) ++cmiss;
         batches_all += all;
         if (!pass) ++culled;
         if (any) {
             ++hits;
-            if (!pass) ++miss;
+            if (!pass || !pass_k) ++miss;
             if (!all) {
                 const double fd = f;
-                const double need = fd > sqrt(r2t) ? (fd * fd - r2t) / (u * wn2) : 0.0;
+                const double need = fd > sqrt(r2t) ? (fd - sqrt(r2t)) / ((double)rp - sqrt(r2t)) : 0.0;
                 if (need > worst) worst = need;
             }
         }
     }
-    printf("f64=%d cases %ld hits %ld misses %ld culled %ld all %ld worst k %.3f\n", f64, n, hits, miss, culled,
+    printf("f64=%d cases %ld hits %ld misses %ld culled %ld all %ld worst margin fraction %.4f\n", f64, n, hits, miss, culled,
            batches_all, worst);
-    return miss != 0;
+    printf("cluster records stricter than a passing member: %ld\n", cmiss);
+    return miss != 0 || cmiss != 0;
 }

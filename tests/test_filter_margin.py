@@ -88,12 +88,16 @@ def test_cone_margin_constant_matches_kernel():
     assert expr in src
     assert expr.replace("r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
     assert "__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f)" in src
+    # cluster records: rp_k >= rp_i + |c_i - C| for every member (the fuzz also checks this directly)
+    assert "rup(R * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (wn + R) + 1e-30)" in src
+    assert "RR * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (Wn + RR) + 1e-30" in \
+        open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
 
 
 @pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
 def test_camera_cone_cull_is_conservative(cone_fuzz_bin, f64):
     """Camera batches: a sphere any ray of the batch hits (Q1, root2 or scalar test) passes the
-    wave's cone cull; margin 64 u |w|^2 in r^2 with >= 4x headroom over the worst case found."""
+    wave's cone cull; the worst case found uses at most a quarter of rp - r (>= 4x headroom)."""
     r = subprocess.run([cone_fuzz_bin, "2000000", str(f64), str(0x2545F4914F6CDD1D + f64)], capture_output=True,
                        text=True, timeout=300)
     fields = r.stdout.split()
@@ -103,7 +107,7 @@ def test_camera_cone_cull_is_conservative(cone_fuzz_bin, f64):
     worst = float(fields[-1])
     assert r.returncode == 0 and misses == 0, r.stdout
     assert hits > 1000000 and culled > 50000, r.stdout   # both sides of tangency are exercised
-    assert worst < 64.0 / 4, r.stdout
+    assert worst < 0.25, r.stdout
 
 
 @pytest.fixture(scope="module")
