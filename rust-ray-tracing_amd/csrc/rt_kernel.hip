@@ -13,12 +13,15 @@
 //     from an atomic counter; up to kSlots pixels in flight).  Every ray's bounce k depends only
 //     on its own state and the counter-based RNG key (sample, pixel, k, stream), so no ray waits
 //     for the others; lane utilisation is ~1.0.
-//   * each sweep tests every live ray against every sphere: spheres stream through the scalar
-//     cache in 64-byte groups (s_load_dwordx16 into SGPRs, a free broadcast to all 64 lanes),
-//     two spheres per packed-FP32 instruction, one branch per group on a sign-bit filter.
-//   * pinhole cameras: primary rays run in full-wave camera batches against a per-launch
-//     camera-origin table (oc and c are the same for every primary ray), hits wait in an LDS
-//     queue for free lanes.
+//   * each sweep finds every sphere the reference could hit through conservative fp32 culls and
+//     runs the reference's exact test on those only: spheres stream through the scalar cache in
+//     64-byte groups (s_load_dwordx16 into SGPRs, a free broadcast to all 64 lanes), two spheres
+//     per packed-FP32 instruction; bounced rays first slab-test 16-sphere cluster boxes, then a
+//     per-sphere distance filter on the clusters some lane may hit (nearest_hit).
+//   * pinhole cameras: primary rays run in full-wave camera batches; a cone around the batch's
+//     rays culls clusters and spheres with lanes as spheres (camera_sweep), survivors get the
+//     exact test from a per-launch camera-origin table (oc and c are the same for every primary
+//     ray); hits wait in an LDS queue for free lanes.
 //   * the reference's positions (its per-bounce stable shuffle) are a function of the per-sample
 //     termination bounces alone; when a pixel's last sample ends, finish_pixel replays them,
 //     applies quirk Q3's buffer read ("retire rule") and sums in the reference's order, so fp64
