@@ -678,10 +678,29 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 // the members of the passing clusters.
 __device__ __forceinline__ float ufl(float x) { return __uint_as_float(__builtin_amdgcn_readfirstlane(__float_as_uint(x))); }
 
+// Wave-wide max of a uint32 through DPP (row_shr scans within each row of 16, then row_bcast:15 and
+// row_bcast:31 carry the row maxima to lane 63): six v_max_u32 with DPP sources, no LDS round trips.
+__device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false));   // row_shr:1
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false));   // row_shr:2
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false));   // row_shr:4
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false));   // row_shr:8
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 template <typename T, bool root2, bool SCALAR>
 __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const uint32_t lane = threadIdx.x & 63u;
     const unsigned long long vm = __ballot(v);
+    // the first records of both levels do not depend on the cone: request them before its setup
+    const auto& q = *cold_args<T>();
+    const float4* cs = (const float4*)__builtin_assume_aligned(q.cull, 16);    // per slot (sweep layout)
+    const float4* cc = (const float4*)__builtin_assume_aligned(q.cullc, 16);   // per cluster
+    const uint32_t nx = 4u * q.n_xg, ncl = 4u * q.n_top;
+    const float4 kPad = {0.0f, 0.0f, 0.0f, -INFINITY};
+    const float4 xw0 = lane < nx ? cs[lane] : kPad, kw0 = lane < ncl ? cc[lane] : kPad;
     const float fdx = v ? (float)d.x : 0.0f, fdy = v ? (float)d.y : 0.0f, fdz = v ? (float)d.z : 0.0f;
     const int l0 = (int)__builtin_ctzll(vm);
     float ax = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(fdx), l0));
@@ -701,19 +720,13 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const float s2 = v ? __builtin_fmaf(cz, cz, __builtin_fmaf(cy, cy, cx * cx)) * __builtin_amdgcn_rcpf(dn2) * (1.0f + 0x1.0p-22f) : 0.0f;
     const float dt = __builtin_fmaf(fdz, az, __builtin_fmaf(fdy, ay, fdx * ax));
     bool all = __ballot(v && !(dt > 0.5f)) != 0ull;   // some ray > 60 deg off the axis (or NaN)
-    uint32_t sm = __float_as_uint(s2);   // non-negative floats (and NaN above +inf) order as integers
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) sm = max(sm, (uint32_t)__shfl_xor((int)sm, o));
-    sm = __builtin_amdgcn_readfirstlane(sm);
+    // non-negative floats (and NaN above +inf) order as integers
+    const uint32_t sm = wave_max_dpp(__float_as_uint(s2));
     const float S = ufl(__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f));
     if (!(S < 0.5f)) all = true;
     const float Cc = ufl(sqrtf(__builtin_fmaf(-S, S, 1.0f)));
-    const auto& q = *cold_args<T>();
-    const float4* cs = (const float4*)__builtin_assume_aligned(q.cull, 16);    // per slot (sweep layout)
-    const float4* cc = (const float4*)__builtin_assume_aligned(q.cullc, 16);   // per cluster
     cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
     cptr<uint32_t> ri = (cptr<uint32_t>)q.ridx;
-    const uint32_t nx = 4u * q.n_xg, ncl = 4u * q.n_top;
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
     T best_t = T(INFINITY);
@@ -729,10 +742,12 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
         const float f = __builtin_fmaf(pp, Cc, -(t * S));
         return wc.w > -INFINITY && (all || !(f > wc.w));   // NaN f passes
     };
-    // the reference's exact test (objects.rs:252-257 on the camera-origin table) for scene index i
-    auto exact = [&](uint32_t i) {
+    // the reference's exact test (objects.rs:252-257 on the camera-origin table) for slot sl; the
+    // scene index (for hit_update's tie rule and the result) comes with it, one round trip
+    auto exact = [&](uint32_t sl) {
         KSTAT(2);
-        const T ocx = cxt[4 * i], ocy = cxt[4 * i + 1], ocz = cxt[4 * i + 2], c = cxt[4 * i + 3];
+        const uint32_t i = ri[sl];
+        const T ocx = cxt[4 * sl], ocy = cxt[4 * sl + 1], ocz = cxt[4 * sl + 2], c = cxt[4 * sl + 3];
         if (v) {
             T hb, disc;
             if constexpr (SCALAR) {   // objects.rs:217-222
@@ -748,17 +763,17 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     };
     // 1. the always-exact spheres (build_layout's leading slots), lanes as spheres
     for (uint32_t base = 0; base < nx; base += 64u) {
-        unsigned long long m = __ballot(base + lane < nx && cone(cs[base + lane]));
+        unsigned long long m = __ballot(base + lane < nx && cone(base == 0 ? xw0 : cs[base + lane]));
         while (m != 0ull) {
             const uint32_t s = base + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            exact(ri[s]);
+            exact(s);
         }
     }
     // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
     // to 4 passing clusters per pass, 16 lanes each
     for (uint32_t cb = 0; cb < ncl; cb += 64u) {
-        unsigned long long M = __ballot(cone(cc[cb + lane]));   // the table is padded to whole 64s
+        unsigned long long M = __ballot(cone(cb == 0 ? kw0 : cc[cb + lane]));   // padded to whole 64s
         while (M != 0ull) {
             uint32_t k[4];
 #pragma unroll
@@ -773,7 +788,7 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
                 const uint32_t b = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1ull;
                 const uint32_t kb = (b >> 4) == 0 ? k[0] : (b >> 4) == 1 ? k[1] : (b >> 4) == 2 ? k[2] : k[3];
-                exact(ri[nx + 16u * kb + (b & 15u)]);
+                exact(nx + 16u * kb + (b & 15u));
             }
         }
     }
@@ -919,11 +934,6 @@ __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* c
         float* out = camf + 16 * fg + 8 * (fj / 2) + (fj % 2);
         out[0] = (float)ocx; out[2] = (float)ocy; out[4] = (float)ocz; out[6] = sc;
     }
-    if (i < n_cull) {   // per-sphere (scene index) AoS copy of the camera-origin record
-        T ex = T(0), ey = T(0), ez = T(0), ec = T(INFINITY);
-        if (i < n_real) { ex = ocx; ey = ocy; ez = ocz; ec = c; }
-        camx[4 * i] = ex; camx[4 * i + 1] = ey; camx[4 * i + 2] = ez; camx[4 * i + 3] = ec;
-    }
     auto rup = [](double v) -> float {   // fp32 >= v; +inf past 1e30 (and for NaN)
         if (!(v < 1e30)) return INFINITY;
         float f = (float)v;
@@ -934,20 +944,26 @@ __global__ void build_cam_table(const T* sph, T* cam, uint32_t n_slots, float* c
         // Cone-cull record of slot i of the sweep layout (camera_sweep): w = c - O in fp32 and
         // rp = sqrt(r^2 (1 + 2^-20) + 64 u |w|^2) + 32 u |w| rounded up (u = 2^-24); +inf (always tested)
         // for non-finite values and under RT_FILTER_OFF, -inf for dummy slots (never pass).
+        // Also the slot's camera-origin record {ocx, ocy, ocz, c} (the exact test of camera_sweep),
+        // computed with the reference's operations as above; a dummy slot gets c = +inf.
         const uint32_t sj = ridx[i];
         float w[3] = {0.0f, 0.0f, 0.0f}, rp = -INFINITY;
+        T ex = T(0), ey = T(0), ez = T(0), ec = T(INFINITY);
         if (sj != 0xFFFFFFFFu) {
             const uint32_t gj = sj / G, jj = sj % G;
             auto atj = [&](uint32_t f) -> uint32_t {
                 return sizeof(T) == 4 ? gj * NE + 8 * (jj / 2) + 2 * f + (jj % 2) : gj * NE + 4 * jj + f;
             };
-            const T wx = sph[atj(0)] - ox, wy = sph[atj(1)] - oy, wz = sph[atj(2)] - oz;   // = -(o - c) exactly
-            const double wn2 = (double)wx * (double)wx + (double)wy * (double)wy + (double)wz * (double)wz;
-            const double r2 = (double)sph[atj(3)];
-            rp = pass_all ? INFINITY : rup(sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30);
-            w[0] = (float)wx; w[1] = (float)wy; w[2] = (float)wz;
+            const T cx = sph[atj(0)], cy = sph[atj(1)], cz = sph[atj(2)], r2 = sph[atj(3)];
+            ex = ox - cx; ey = oy - cy; ez = oz - cz;
+            ec = SCALAR ? ((ex * ex + ey * ey) + ez * ez) - r2 : fma(ez, ez, fma(ey, ey, ex * ex)) - r2;
+            const double wn2 = (double)ex * (double)ex + (double)ey * (double)ey + (double)ez * (double)ez;
+            rp = pass_all ? INFINITY
+                          : rup(sqrt((double)r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30);
+            w[0] = -(float)ex; w[1] = -(float)ey; w[2] = -(float)ez;   // c - O = -(O - c) exactly
         }
         cull[4 * i] = w[0]; cull[4 * i + 1] = w[1]; cull[4 * i + 2] = w[2]; cull[4 * i + 3] = rp;
+        camx[4 * i] = ex; camx[4 * i + 1] = ey; camx[4 * i + 2] = ez; camx[4 * i + 3] = ec;
     }
     if (i < n_clp) {
         // Cluster record: W = C - O and rp_k = R (1 + 2^-20) + (2^-9 + 2^-16) (|W| + R) (C, R: the
@@ -1279,6 +1295,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
+#ifdef RT_EXP_DUP_FINISH   // timing experiment: finish_pixel twice (idempotent)
+                (void)finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
+                wave_mem_sync();
+#endif
                 const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
                                                          s_hist[wave]);
                 if (lane == 0) wcount[wave][2] += K;
@@ -1295,6 +1315,23 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const unsigned long long vm = __ballot(v);
         if (vm == 0ull) return false;
         V3<T> bd = mk(T(0), T(0), T(0));
+#ifdef RT_EXP_DUP_CAMRAY   // timing experiment: the camera ray twice (same result)
+        if (v) {
+            uint32_t bsid2 = bsid;
+            asm volatile("" : "+v"(bsid2));
+            const U4 r = [&] {
+                const auto& q0 = *cold_args<T>();
+                return philox(bsid2, bpix, 0u, 0u, q0.k0, q0.k1);
+            }();
+            const auto& q = *cold_args_after<T>(r.a ^ r.b);
+            const T s1 = ((T)bcol + u01a(r, T(0))) / (T)q.W;
+            const T s2 = ((T)brow + u01b(r, T(0))) / (T)q.H;
+            const V3<T> vu = mk(q.vu[0], q.vu[1], q.vu[2]), vv = mk(q.vv[0], q.vv[1], q.vv[2]);
+            const V3<T> pc = add(mk(q.ulc[0], q.ulc[1], q.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
+            const V3<T> bd2 = unit(sub(pc, mk(q.center[0], q.center[1], q.center[2])));
+            asm volatile("" ::"v"(bd2.x), "v"(bd2.y), "v"(bd2.z));
+        }
+#endif
         if (v) {   // Camera::get_ray (ray_tracing.rs:77-89) with origin == centre
             const U4 r = [&] {
                 const auto& q0 = *cold_args<T>();
@@ -1926,8 +1963,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     HIPCHK(hipMalloc(&c->cam64, g64.size() * sizeof(double)));
     HIPCHK(hipMalloc(&c->cam32, g32.size() * sizeof(float)));
     c->n_cull = (s->n_spheres + 63u) / 64u * 64u + 64u;
-    HIPCHK(hipMalloc(&c->camx64, (size_t)4 * c->n_cull * sizeof(double)));
-    HIPCHK(hipMalloc(&c->camx32, (size_t)4 * c->n_cull * sizeof(float)));
+    HIPCHK(hipMalloc(&c->camx64, (size_t)4 * c->n_cslots * sizeof(double)));
+    HIPCHK(hipMalloc(&c->camx32, (size_t)4 * c->n_cslots * sizeof(float)));
     HIPCHK(hipMalloc(&c->cull64, (size_t)4 * c->n_cslots * sizeof(float)));
     HIPCHK(hipMalloc(&c->cull32, (size_t)4 * c->n_cslots * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;

@@ -84,9 +84,9 @@ def cone_fuzz_bin(tmp_path_factory):
 
 def test_cone_margin_constant_matches_kernel():
     src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
-    expr = "sqrt(r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30"   # 64 u, 32 u
+    expr = "sqrt((double)r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30"   # 64 u, 32 u
     assert expr in src
-    assert expr.replace("r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
+    assert expr.replace("(double)r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
     assert "__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f)" in src
     # cluster records: rp_k >= rp_i + |c_i - C| for every member (the fuzz also checks this directly)
     assert "rup(R * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (wn + R) + 1e-30)" in src
