@@ -127,6 +127,7 @@ template <typename T> struct KParams {
     const T* rsph;
     const float* rfsph;
     const float* ftop;
+    const float* fsup;         // super boxes (4 clusters each), 4 per group
     const uint32_t* ridx;
     uint32_t n_top, n_xg;
 };
@@ -635,20 +636,33 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // test.  The phases never hold both SGPR pipelines at once (no SGPR spills).
         const uint32_t nxg = qa.n_xg, ntop = qa.n_top;
         for (uint32_t g = 0; g < nxg; ++g) exact4(g);
+        // Three levels: super boxes (4 clusters each, 4 per group) per chunk of 32 supers, then the
+        // passing supers' cluster boxes (one group each), then the passing clusters' sphere groups.
         cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 32);
-        for (uint32_t t0 = 0; t0 < ntop; t0 += 8u) {
-            uint32_t mask = 0;
-            box_loop(ft + kBoxFloats * t0, min(8u, ntop - t0), [&](const BoxGroup& cur, uint32_t t) {
+        cptr<float> fs = (cptr<float>)__builtin_assume_aligned(qa.fsup, 32);
+        const uint32_t nsg = (ntop + 3u) / 4u;   // super groups (ntop supers, one per cluster top group)
+        for (uint32_t t0 = 0; t0 < nsg; t0 += 8u) {
+            uint32_t smask = 0;
+            box_loop(fs + kBoxFloats * t0, min(8u, nsg - t0), [&](const BoxGroup& cur, uint32_t t) {
                 KSTAT(5);
-                mask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
+                smask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
             });
-            while (mask != 0u) {
-                const uint32_t g0 = nxg + 4u * (4u * t0 + (uint32_t)__builtin_ctz(mask));
-                mask &= mask - 1u;
-                KSTAT(4);
-                sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
-                    if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
-                });
+            while (smask != 0u) {
+                const uint32_t sup = 4u * t0 + (uint32_t)__builtin_ctz(smask);
+                smask &= smask - 1u;
+                // padding supers past the last one are empty boxes; a degenerate lane (all box times
+                // NaN) passes them, and they have no cluster boxes behind them
+                if (sup >= ntop) break;
+                KSTAT(5);
+                uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
+                while (mask != 0u) {
+                    const uint32_t g0 = nxg + 4u * (4u * sup + (uint32_t)__builtin_ctz(mask));
+                    mask &= mask - 1u;
+                    KSTAT(4);
+                    sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
+                        if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
+                    });
+                }
             }
         }
 #endif
@@ -1512,6 +1526,7 @@ struct rt_context {
     void* rsph64 = nullptr; void* rsph32 = nullptr; // general sweep: slot-order exact groups
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
+    void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
     uint32_t* ridx = nullptr;
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
     void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
@@ -1603,6 +1618,8 @@ static void free_scene(rt_context* c) {
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
     (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
+    (void)hipFree(c->sup64); (void)hipFree(c->sup32);
+    c->sup64 = c->sup32 = nullptr;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
     c->clus64 = c->clus32 = c->cullc64 = c->cullc32 = nullptr;
     c->n_cslots = c->n_clp = 0;
@@ -1810,7 +1827,7 @@ static SweepLayout build_layout(const rt_scene* s) {
 template <typename T>
 static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec, const SweepLayout& L,
                        std::vector<T>& rgrp, std::vector<float>& rfgrp, std::vector<float>& top, float& cmax,
-                       float& r2max) {
+                       float& r2max, std::vector<float>& sup) {
     auto up32 = [](double v) -> float {
         float f = (float)v;
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
@@ -1866,6 +1883,39 @@ static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec
         const size_t tg = k / 4, j = k % 4;
         for (int f = 0; f < 6; ++f) top[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
     }
+    // Super boxes: the union of the 4 cluster boxes of each top group, same rounding; 4 per group,
+    // padded with empty boxes plus one empty group (prefetch target).
+    const size_t nsup = nc / 4, nsg = (nsup + 3) / 4;
+    sup.assign((size_t)kBoxFloats * (nsg + 1), 0.0f);
+    for (size_t k = 0; k < 4 * (nsg + 1); ++k) {
+        float b[6] = {0.0f, 0.0f, 0.0f, -INFINITY, -INFINITY, -INFINITY};
+        if (k < nsup) {
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            bool inf = false, any = false;
+            for (size_t j = 0; j < 4; ++j) {
+                const float* t = &top[kBoxFloats * k + 12 * (j / 2) + (j % 2)];
+                if (!(t[6] > -INFINITY)) continue;   // empty cluster
+                any = true;
+                for (int a = 0; a < 3; ++a) {
+                    if (!(t[6 + 2 * a] < INFINITY)) inf = true;
+                    lo[a] = std::min(lo[a], (double)t[2 * a] - (double)t[6 + 2 * a]);
+                    hi[a] = std::max(hi[a], (double)t[2 * a] + (double)t[6 + 2 * a]);
+                }
+            }
+            if (any) {
+                double c1 = 0.0;
+                for (int a = 0; a < 3; ++a) {
+                    b[a] = inf ? 0.0f : (float)(0.5 * (lo[a] + hi[a]));
+                    const double h = std::max(hi[a] - (double)b[a], (double)b[a] - lo[a]);
+                    b[3 + a] = inf ? INFINITY : up32(h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a]));
+                    c1 += std::fabs((double)b[a]) + (double)b[3 + a];
+                }
+                if (!inf) cm = std::max(cm, c1);
+            }
+        }
+        const size_t tg = k / 4, j = k % 4;
+        for (int f = 0; f < 6; ++f) sup[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
+    }
     cmax = up32(cm);
     (void)r2max;
 }
@@ -1905,9 +1955,11 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
         const SweepLayout L = build_layout(s);
-        std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32;
-        pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64);
-        pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32);
+        std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32, s64, s32;
+        pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64, s64);
+        pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32, s32);
+        if ((rc = up(&c->sup64, s64.data(), s64.size() * sizeof(float))) != RT_OK) return rc;
+        if ((rc = up(&c->sup32, s32.data(), s32.size() * sizeof(float))) != RT_OK) return rc;
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
         // slot -> scene index (0xFFFFFFFF: dummy), padded past the last cluster by one block of 64
@@ -2014,6 +2066,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.rsph = (const T*)(f64 ? c->rsph64 : c->rsph32);
     p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
     p.ftop = (const float*)(f64 ? c->top64 : c->top32);
+    p.fsup = (const float*)(f64 ? c->sup64 : c->sup32);
     p.ridx = c->ridx;
     p.n_top = c->n_top;
     p.n_xg = c->n_xg;
