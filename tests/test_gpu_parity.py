@@ -234,6 +234,38 @@ def test_full_size_configs(renderer, config, flags):
     assert 0.2 < lin.mean() < 0.9 and 1.0 < st.ray_segments / (w * h * spp) < 4.0
 
 
+@pytest.mark.parametrize("w,h,spp,depth,stride,flags", [
+    (1280, 720, 4, 3, 1, abi.RT_FLAG_F32),   # 921 600 items: 16/8/4/2/1-item blocks in all 16 partitions
+    (1920, 1080, 4, 2, 1, 0),
+    (1920, 1080, 4, 2, 7, abi.RT_FLAG_F32),  # a row-strided shard (155 rows)
+    (7, 3, 8, 4, 1, abi.RT_FLAG_F32),        # fewer items than partitions: empty partitions
+    (1, 1, 4, 4, 1, 0),
+])
+def test_schedule_covers_every_pixel(renderer, scene_100, w, h, spp, depth, stride, flags):
+    """The work schedule (pixel blocks claimed from 16 partition counters, guided block sizes,
+    stealing) renders every pixel of the range exactly once: the whole frame is bit-identical to
+    the oracle, pixel for pixel, and the sample count is exact."""
+    cam = cam_for(w, h)
+    tile = rt.parallel.shard_range(w, h, stride, 3 % stride) if stride > 1 else None
+    rgb, lin, st, rc = gpu(renderer, scene_100, cam, depth, spp, SEED, flags, tile=tile)
+    assert rc == 0
+    if tile is None:
+        px = None
+        n = w * h
+    else:
+        rows = np.arange(3 % stride, h, stride)
+        px = (rows[:, None] * w + np.arange(w)[None, :]).reshape(-1).astype(np.uint32)
+        n = len(px)
+    assert st.samples == n * spp
+    rgb_o, lin_o, segs_o, _ = oracle_render(scene_100, cam, depth, spp, SEED, 0, pixels=px,
+                                            precision="f32" if flags & abi.RT_FLAG_F32 else "f64")
+    assert lin.shape == lin_o.shape
+    bad = np.argwhere((lin != lin_o).any(axis=1))
+    assert bad.size == 0, f"{len(bad)} pixels differ, first {bad[0][0]}"
+    np.testing.assert_array_equal(rgb, rgb_o)
+    assert st.ray_segments == segs_o
+
+
 # ---------------------------------------------------------------- the CLI (main.rs) end to end
 def test_cli_renders_config_a_from_toml(tmp_path):
     """rt-render reads scene.toml, renders on the GPU, writes PNG and PPM (src/main.rs:27-74); the
