@@ -1105,6 +1105,16 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
+#ifdef RT_EXP_SKIP_REDUCE
+constexpr bool kSkipReduce = true;
+#else
+constexpr bool kSkipReduce = false;
+#endif
+#ifdef RT_EXP_SKIP_INIT
+constexpr bool kSkipInit = true;   // timing experiment only: results are wrong
+#else
+constexpr bool kSkipInit = false;
+#endif
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item,
                                                           uint32_t* hist) {
@@ -1116,7 +1126,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424) with a zero
     // primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel == 0).
     // Positions [0, spp) start at 0 (a ray still enabled at the end contributes black).
-    if (MODE == kModeV2) {
+    if (MODE == kModeV2 && !kSkipInit) {
         const V3<T> s0 = sky(T(0.0));
         const bool white0 = q.s_sel == 0u;
         for (uint32_t qi = lane; qi < P; qi += 64u) {
@@ -1136,11 +1146,107 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         K = min(depth, __builtin_amdgcn_readfirstlane(wave_max(me)) + 1u);
     }
     wave_mem_sync();
+    // One pass over the samples (K <= 64, the common case): lane k holds the per-bounce counts, so
+    // every sample finds its positions from running counts and ballots over its own chunk of 64.
+    // Sample s, terminated at bounce k = e_s < K, sat at pold = #{s' < s : e_s' >= k} during bounce
+    // k and moves to pnew = n_{k+1} + #{s' < s : e_s' == k} in the sorted copy (n_k = #{e >= k});
+    // the retire rule then picks which of the two holds its value.  The same writes
+    // as the per-bounce loop below, which rescans the records once per bounce (one memory round trip
+    // per bounce and chunk; 12 % of config C's time).
+    bool replayed = false;
+#if !defined(RT_EXP_SKIP_REPLAY) && !defined(RT_EXP_OLD_REPLAY)
+    if (MODE == kModeV2 && K > 0u && K <= 64u) {
+        replayed = true;
+        hist[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+        auto load_e = [&](uint32_t b, uint32_t (&ev)[8]) {   // e of samples b .. b+511 (8 chunks)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t i = b + 64u * u + lane;
+                ev[u] = i < spp ? sc.e(s, i) : 0xFFFFFFFFu;
+            }
+        };
+        for (uint32_t b = 0; b < spp; b += 512u) {   // histogram of e (e < K)
+            uint32_t ev[8];
+            load_e(b, ev);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (ev[u] < K) atomicAdd(&hist[ev[u]], 1u);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t H = hist[lane];
+        uint32_t pre = H;   // inclusive prefix sum over lanes: #{e <= lane}
+#pragma unroll
+        for (uint32_t o = 1; o < 64u; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, o);
+            if (lane >= o) pre += y;
+        }
+        const uint32_t n_l = spp - (pre - H), nn_l = spp - pre;   // n_k, n_{k+1} for k = lane
+        uint32_t cge = 0, ceq = 0;   // lane k: samples of the earlier chunks with e >= k, e == k
+        for (uint32_t b = 0; b < spp; b += 512u) {   // the samples in order, 64 at a time
+            uint32_t ev[8];
+            load_e(b, ev);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                if (b + 64u * u >= spp) break;
+                const uint32_t i = b + 64u * u + lane, e = ev[u];
+                const bool in = i < spp, ret = e < K;
+                V3<T> c = mk(T(0), T(0), T(0));
+                if (ret) c = mk(sc.c(s, 0, i), sc.c(s, 1, i), sc.c(s, 2, i));
+                unsigned long long rem = __ballot(ret);
+                uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nk = 0, nn = 0;
+#ifdef RT_EXP_NO_POSLOOP   // timing experiment only: results are wrong
+                rem = 0ull; pold = i; pnew = i;
+#endif
+                while (rem != 0ull) {   // one pass per distinct bounce k among the chunk's retiring lanes
+                    const uint32_t k = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(rem));
+                    const unsigned long long bge = __ballot(in && e >= k), beq = __ballot(e == k);
+                    const uint32_t cnt = (uint32_t)__popcll(beq);
+                    const uint32_t cg = __builtin_amdgcn_readlane(cge, (int)k), cq = __builtin_amdgcn_readlane(ceq, (int)k);
+                    const uint32_t n0 = __builtin_amdgcn_readlane(n_l, (int)k), n1 = __builtin_amdgcn_readlane(nn_l, (int)k);
+                    if (e == k) {
+                        pold = cg + (uint32_t)__popcll(bge & lt_mask);
+                        pnew = n1 + cq + (uint32_t)__popcll(beq & lt_mask);
+                        nk = n0;
+                        nn = n1;
+                    }
+                    if (lane <= k) gadd += cnt;   // lane j: this chunk's #{e >= j}
+                    if (lane == k) hc = cnt;
+                    rem &= ~beq;
+                }
+                cge += gadd + (uint32_t)__popcll(__ballot(in && e >= K));
+                ceq += hc;
+                const uint32_t ek = ret ? e : 0u;
+#ifdef RT_EXP_NO_RWRITES   // timing experiment only: results are wrong
+                if (ret && pold == 0xFFFFFFFFu) {
+#else
+                if (ret) {
+#endif
+                    const uint32_t Lk = (nk + 3u) / 4u, Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
+                    const uint32_t lo = 4u * Lnext, hi = 4u * Lk;   // positions retiring at bounce e
+                    const bool U = q.s_sel == (ek & 1u);
+                    const bool w_old = U && pold >= lo && pold < hi;
+                    const bool w_new = !U || pnew < lo || pnew >= hi;
+                    if (w_old || w_new) {
+                        const uint32_t q1 = w_old ? pold : pnew;
+                        const V3<T> sk = sky(sc.y(s, q1));
+                        sc.v(0, q1) = c.x * sk.x; sc.v(1, q1) = c.y * sk.y; sc.v(2, q1) = c.z * sk.z;
+                    }
+                    if (w_old && w_new) {
+                        const V3<T> sk = sky(sc.y(s, pnew));
+                        sc.v(0, pnew) = c.x * sk.x; sc.v(1, pnew) = c.y * sk.y; sc.v(2, pnew) = c.z * sk.z;
+                    }
+                }
+            }
+        }
+    }
+#endif
     uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
 #ifdef RT_EXP_SKIP_REPLAY
     for (uint32_t k = 0; k < 0u; ++k) {   // timing experiment only: results are wrong
 #else
-    for (uint32_t k = 0; k < (MODE == kModeV2 ? K : 0u); ++k) {
+    for (uint32_t k = 0; k < (MODE == kModeV2 && !replayed ? K : 0u); ++k) {
 #endif
         if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
             kb = k;
@@ -1201,7 +1307,11 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         else return pos < spp ? sc.c(s, ch, pos) : T(0.0);
     };
     T acc = T(0.0);
+#ifdef RT_EXP_SKIP_REDUCE   // timing experiment only: results are wrong
+    if (false) {
+#else
     if (MODE == kModeScalar) {
+#endif
         if (lane < 3u) {
             uint32_t i = 0;
             for (; i + 16 <= spp; i += 16) {
@@ -1213,7 +1323,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             }
             for (; i < spp; ++i) acc = acc + sc.c(s, lane, i);
         }
-    } else if (lane < 12u) {
+    } else if (lane < 12u && !kSkipReduce) {
         const uint32_t ch = lane >> 2, l = lane & 3u;
         uint32_t j = 0;
         for (; j + 16 <= C; j += 16) {
