@@ -232,7 +232,8 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
 // pairs).  The two pairs are interleaved so that no packed result is read by the next instruction
 // (the one-wait-state packed-FP32 read hazard the compiler pads with s_nop).  14 packed ops, then
 // v_and3 + v_bitop3 on the sign bits.
-__device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3) {
+__device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3, uint32_t& s0,
+                                                 uint32_t& s1) {
     const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
     const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
     f2 a0, b0, a1, b1, r0, r1;
@@ -254,9 +255,11 @@ __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 
         : [a0] "=&v"(a0), [b0] "=&v"(b0), [a1] "=&v"(a1), [b1] "=&v"(b1), [r0] "=&v"(r0), [r1] "=&v"(r1)
         : [cx0] "s"(cx0), [cy0] "s"(cy0), [cz0] "s"(cz0), [rr0] "s"(rr0), [cx1] "s"(cx1), [cy1] "s"(cy1),
           [cz1] "s"(cz1), [rr1] "s"(rr1), [K0] "v"(K0), [K1] "v"(K1), [K2] "v"(K2), [K3] "v"(K3));
-    // ~(D0 & D1 & D2 & D3): sign set iff some sphere of the group passes (D >= +0)
-    const uint32_t t = __float_as_uint(r0.x) & __float_as_uint(r0.y) & __float_as_uint(r1.x);
-    return __builtin_amdgcn_bitop3_b32(t, __float_as_uint(r1.y), 0u, 0x3F);
+    // ~(D0 & D1 & D2 & D3): sign set iff some sphere of the group passes (D >= +0); s0, s1: the
+    // same per sphere pair, un-negated (sign clear iff a sphere of the pair passes)
+    s0 = __float_as_uint(r0.x) & __float_as_uint(r0.y);
+    s1 = __float_as_uint(r1.x) & __float_as_uint(r1.y);
+    return ~(s0 & s1);
 }
 
 // The camera-batch filter for one 4-sphere group (nearest_hit, CAMT under Q1): per sphere pair
@@ -568,8 +571,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
         const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, 0.0f}, K3 = {-oe1, -oe2};
         const f2 B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, 0.0f};
-        // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222).
-        auto exact4 = [&](uint32_t g) {
+        // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
+        // the sphere pairs set in `pairs` (bit q: spheres 4g+2q, 4g+2q+1; wave-uniform).
+        auto exact4 = [&](uint32_t g, uint32_t pairs = 3u) {
             KSTAT(0);
             if constexpr (sizeof(T) == 4) {
                 // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two
@@ -578,32 +582,32 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
                 const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
                 const f2 na = {-a, -a};
-                f2 hb[2], disc[2];
+                const Q4 si = sidx(g);
 #pragma unroll
                 for (uint32_t q = 0; q < 2; ++q) {
+                    if (!((pairs >> q) & 1u)) continue;
+                    f2 hb, disc;
                     const T* v = &cur.v[8 * q];
                     const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, r2 = {v[6], v[7]};
                     const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
                     if constexpr (SCALAR) {                                           // objects.rs:217-222
-                        hb[q] = (ocx * dx + ocy * dy) + ocz * dz;
+                        hb = (ocx * dx + ocy * dy) + ocz * dz;
                         const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
-                        disc[q] = hb[q] * hb[q] - (-na) * c;
+                        disc = hb * hb - (-na) * c;
                     } else {
-                        hb[q] = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));               // :255
+                        hb = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));                  // :255
                         const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;  // :256
-                        disc[q] = fma2(hb[q], hb[q], na * c);                         // :257
+                        disc = fma2(hb, hb, na * c);                                  // :257
                     }
+                    if (cand_f(hb.x, disc.x)) hit(hb.x, disc.x, q ? si.z : si.x);
+                    if (cand_f(hb.y, disc.y)) hit(hb.y, disc.y, q ? si.w : si.y);
                 }
-                const Q4 si = sidx(g);
-                if (cand_f(hb[0].x, disc[0].x)) hit(hb[0].x, disc[0].x, si.x);
-                if (cand_f(hb[0].y, disc[0].y)) hit(hb[0].y, disc[0].y, si.y);
-                if (cand_f(hb[1].x, disc[1].x)) hit(hb[1].x, disc[1].x, si.z);
-                if (cand_f(hb[1].y, disc[1].y)) hit(hb[1].y, disc[1].y, si.w);
             } else {
                 const SphGroup<T> c0 = load_group(fe, 2 * g), c1 = load_group(fe, 2 * g + 1);
                 T hb[4], disc[4];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j) {
+                    if (!((pairs >> (j >> 1)) & 1u)) continue;
                     const T* v = j < 2 ? &c0.v[4 * j] : &c1.v[4 * (j - 2)];
                     const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
                     if constexpr (SCALAR) {                                    // objects.rs:217-222
@@ -619,12 +623,13 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 const uint32_t sv[4] = {si.x, si.y, si.z, si.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    if (cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
+                    if (((pairs >> (j >> 1)) & 1u) && cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
             }
         };
 #ifdef RT_EXP_FLAT_SWEEP
         auto group = [&](const SphGroup<float>& cur, uint32_t g) {
-            if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g);
+            uint32_t s0, s1;
+            if (is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) exact4(g);
         };
         sphere_loop(ff, ngf, group);
 #else
@@ -660,7 +665,17 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     mask &= mask - 1u;
                     KSTAT(4);
                     sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
-                        if (is_cand(filter_group(cur, K0, K1, K2, K3))) exact4(g0 + g);
+                        uint32_t s0, s1;
+                        if (is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) {
+                            // only the sphere pairs some lane passes (one compare each, taken groups only)
+                            uint32_t pairs = 3u;
+#ifndef RT_EXP_PAIRS_F64
+                            if constexpr (sizeof(T) == 4)
+#endif
+                                pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
+                                        (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
+                            exact4(g0 + g, pairs);
+                        }
                     });
                 }
             }
