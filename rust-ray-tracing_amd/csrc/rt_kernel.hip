@@ -129,7 +129,7 @@ template <typename T> struct KParams {
     const float* ftop;
     const float* fsup;         // super boxes (4 clusters each), 4 per group
     const uint32_t* ridx;
-    uint32_t n_top, n_xg;
+    uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
 
 constexpr int kSegShards = 256;
@@ -640,7 +640,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // walks the set clusters' groups with the per-sphere filter and, where it passes, the exact
         // test.  The phases never hold both SGPR pipelines at once (no SGPR spills).
         const uint32_t nxg = qa.n_xg, ntop = qa.n_top;
-        for (uint32_t g = 0; g < nxg; ++g) exact4(g);
+        // the always-exact groups; fp32 skips a pair of dummies at the end (the ground sphere's group
+        // at config C: ground + 3 dummies); in fp64 the variable pair mask costs VGPR spills at W4
+        for (uint32_t g = 0; g < nxg; ++g) exact4(g, sizeof(T) == 4 && 4u * g + 2u >= qa.n_xs ? 1u : 3u);
         // Three levels: super boxes (4 clusters each, 4 per group) per chunk of 32 supers, then the
         // passing supers' cluster boxes (one group each), then the passing clusters' sphere groups.
         cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 32);
@@ -1731,7 +1733,7 @@ struct rt_context {
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
     void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
     uint32_t n_cslots = 0, n_clp = 0;                 // slot-order cull records; cluster records (x64)
-    uint32_t n_top = 0, n_xg = 0;
+    uint32_t n_top = 0, n_xg = 0, n_xs = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
     uint32_t* smat = nullptr;
@@ -1825,7 +1827,7 @@ static void free_scene(rt_context* c) {
     c->n_cslots = c->n_clp = 0;
     c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
     c->ridx = nullptr;
-    c->n_top = c->n_xg = 0;
+    c->n_top = c->n_xg = c->n_xs = 0;
     (void)hipFree(c->smat);
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
@@ -1963,6 +1965,7 @@ struct SweepLayout {
     std::vector<int32_t> slot;                   // slot -> scene index, -1 = dummy (4 slots per group)
     std::vector<std::vector<uint32_t>> members;  // per cluster (count padded to a multiple of 4)
     uint32_t n_xg = 0;                           // leading groups of always-exact spheres
+    uint32_t n_xs = 0;                           // always-exact spheres (slots 0 .. n_xs-1)
 };
 static SweepLayout build_layout(const rt_scene* s) {
     const uint32_t n = s->n_spheres;
@@ -1983,6 +1986,7 @@ static SweepLayout build_layout(const rt_scene* s) {
     }
     SweepLayout L;
     for (uint32_t i : exact) L.slot.push_back((int32_t)i);
+    L.n_xs = (uint32_t)exact.size();
     while (L.slot.size() % 4) L.slot.push_back(-1);
     L.n_xg = (uint32_t)(L.slot.size() / 4);
     // k-d split; the left part takes a multiple of kClusterMax so that leaves stay full
@@ -2162,6 +2166,7 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->sup32, s32.data(), s32.size() * sizeof(float))) != RT_OK) return rc;
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
+        c->n_xs = L.n_xs;
         // slot -> scene index (0xFFFFFFFF: dummy), padded past the last cluster by one block of 64
         // (the camera sweep's empty quarters read the slots of cluster index n_clusters)
         const uint32_t ncl = (uint32_t)L.members.size();
@@ -2270,6 +2275,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.ridx = c->ridx;
     p.n_top = c->n_top;
     p.n_xg = c->n_xg;
+    p.n_xs = c->n_xs;
     p.f_cmax = f64 ? c->f_cmax64 : c->f_cmax32;
     p.f_r2max = f64 ? c->f_r2max64 : c->f_r2max32;
     p.f_r2min = f64 ? c->f_r2min64 : c->f_r2min32;
