@@ -107,6 +107,7 @@ template <typename T> struct KParams {
     unsigned long long* segs;  // kSegShards counters, one per 128-B line
     uint32_t* err;
     uint32_t* counter;         // next block of work items (guided_block)
+    uint32_t blk_g;            // largest block (a power of two <= kMaxBlock; launch_t)
     uint32_t n_items;
     char* scratch;             // per-wave scratch regions
     size_t scratch_stride;
@@ -1084,8 +1085,14 @@ struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, dra
 //     whatever its spp.
 //   * The tail is the other cost: a block is worked off by the 4 waves of one workgroup, and a late
 //     16-pixel block of long glass paths at 512 spp, claimed by one wave, ran ~15 ms past the rest.
-//     G (a power of two <= kMaxBlock) keeps a block within kBlockSamples samples.
+//     G (a power of two <= kMaxBlock, chosen per launch by the host) keeps a block within
+//     kBlockSamples samples and within 1/kBlockShare of a wave's share of the pixels.  The second
+//     bound is for small launches: 8-way row shards of C (~50 pixels per wave) with G = 16 ended
+//     with one workgroup on 16 adjacent glass pixels, 8.2 ms against 5.7 ideal; with G = 2 they
+//     scale perfectly.  Scattering the claim order instead (pixels or 16-pixel tiles) cost 4-5 % at
+//     config C: waves on a CU then walk different clusters, and the sphere data thrash the scalar cache.
 constexpr uint32_t kMaxBlock = 16;
+constexpr uint32_t kBlockShare = 24;
 #ifndef RT_EXP_BLOCK_SAMPLES
 #define RT_EXP_BLOCK_SAMPLES 8192
 #endif
@@ -1440,11 +1447,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                             pv = old;
                         }
                         if (it == 0xFFFFFFFFu) {
-                            const uint32_t gs = max(1u, kBlockSamples / spp);   // G: largest power of two <= min(gs, kMaxBlock)
-                            const uint32_t G = gs >= kMaxBlock ? kMaxBlock : 1u << (31 - __builtin_clz(gs));
                             const uint32_t j = atomicAdd(q.counter, 1u);
                             uint32_t b0 = 0, b1 = 0;
-                            if (guided_block(q.n_items, max(1u, kTMul * gridDim.x), G, j, b0, b1)) {
+                            if (guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, j, b0, b1)) {
                                 it = b0;
                                 if (b1 > b0 + 1u &&
                                     atomicCAS(&s_pool, pv, ((unsigned long long)(b0 + 1u) << 32) | b1) != pv) {
@@ -2355,6 +2360,14 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
     const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
     if (nblocks > need) nblocks = need;
+    {   // G: the largest power of two <= min(kMaxBlock, kBlockSamples / spp, pixels per wave / kBlockShare)
+        const uint64_t per_wave = (uint64_t)p.n_items / (4u * nblocks);
+        const uint64_t g = std::max<uint64_t>(1u, std::min<uint64_t>({(uint64_t)kMaxBlock, kBlockSamples / spp,
+                                                                      per_wave / kBlockShare}));
+        uint32_t G = 1;
+        while (2u * G <= g) G *= 2u;
+        p.blk_g = G;
+    }
     p.vbytes = paths_vbytes(p.P, sizeof(T));
     p.sbytes = paths_sbytes(p.P, sizeof(T));
     p.scratch_stride = (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
