@@ -138,6 +138,10 @@ constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
 constexpr int kWavesF32 = 5;   // default min-waves-per-SIMD targets (measured sweep)
 constexpr int kWavesF64 = 4;
+// fp32 launches whose samples per resident wave at W6 reach this run at W6: +0.9 % on a whole frame of
+// config C, but the smaller per-wave share of an 8-way shard leaves a tail (5.62 -> 6.14 ms), so W5 there.
+constexpr int kWavesF32Big = 6;
+constexpr uint64_t kBigWaveSamples = 32768;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
@@ -2351,7 +2355,10 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // Persistent grid: as many 4-wave workgroups as stay resident, never more waves than pixels.
     // Minimum waves per SIMD the register allocation targets (RT_WAVES overrides; experiments).
     static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
-    const int W = waves_env ? waves_env : (sizeof(T) == 4 ? kWavesF32 : kWavesF64);
+    const uint64_t big_samples = (uint64_t)c->n_cu * 4u * kWavesF32Big * kBigWaveSamples;
+    const int W = waves_env ? waves_env
+                : sizeof(T) == 8 ? kWavesF64
+                : (uint64_t)rg.row_count * rg.col_count * spp >= big_samples ? kWavesF32Big : kWavesF32;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
     void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W) : pick_kernel<T, false>(flags, W);
