@@ -7,19 +7,23 @@ One step = one full frame of config C (1920x1080, 500 spheres, 512 spp, 50 bounc
 renders its row-interleaved shard (rows r, r+N, ...) with the HIP megakernel, then rank 0 gathers
 the RGB8 shards over RCCL and re-interleaves them (the north star's tiles + gather; total work is
 fixed as N grows -> "scaling": "strong").  Inputs (scene SoA, camera) are resident in HBM before
-the timed region.  Rank 0 prints one JSON line.
+the timed region.  Rank 0 prints one JSON line.  After the headline leg the same steps run in the
+other precision (fp64 = the reference's arithmetic when the headline is fp32), timed the same way,
+under the line's "f64" / "f32" key.
 
-roofline: the trace kernel is VALU-issue-bound (no MFMA; HBM traffic ~5 % of bandwidth).
-  algorithmic FLOP per launch = 17 * n_spheres * ray_segments   (the reference's
-  mandatory 17-FLOP sphere test per segment and sphere; segments counted in-kernel), achieved = that /
-  average launch duration (HIP events on the launch stream), peak = the packed-FP32 VALU peak for
-  both dtypes: fp64 rays also sweep the spheres with the packed-FP32 filters, fp64
-  arithmetic is only used on filter candidates.  The filters spend fewer instructions per (ray,
-  sphere) than the 17-FLOP test, so this frac is an effective (brute-force-equivalent) rate; the
-  physical bound is VALU issue, reported as valu_issue_frac = VALU instructions per launch (PMC,
-  profiles/traffic.json) * 4 cycles / (1024 SIMDs * launch time * 2.4 GHz).
-cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>) on this host's
-  cores over a bounded strided pixel sample of the same workload.
+roofline: the trace kernel is bound by VALU issue (no MFMA; HBM is not binding).
+  executed FLOP per launch = 64 lanes x the FLOP per lane of every wave-level cull and exact test the
+  kernel ran (in-kernel counters, rt_stats.box_groups .. camera_exact_tests; per-test FLOP in
+  include/rt_mi355x.h), split fp32 / fp64; achieved = that / the average launch duration (HIP events
+  around each launch on its stream); peak = 157.3 TF fp32, 78.6 TF fp64 (MI355X vector peaks),
+  blended by the FLOP mix; frac = achieved / peak <= 1.  The reference's brute-force work (17 FLOP
+  per ray segment and sphere) is reported separately as brute_force_equiv: the culls
+  skip most of it, so its "rate" exceeds the chip's peak and says how much work is avoided.
+  valu_busy and traffic come from rocprofv3 PMC passes of this bench (profiles/pmc.json, with the
+  commit they were collected at).
+cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>), built
+  -march=native on this host, on every core this process may use (affinity, capped by the cgroup's
+  CPU quota), over a bounded strided pixel sample of the same workload.
 """
 import argparse
 import ctypes
@@ -31,9 +35,8 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "rust-ray-tracing_amd"))
 
-FP32_VALU_PEAK_TF = 157.3   # MI355X_MICROARCH.md chip table (packed FP32 vector)
-N_SIMD, CLOCK_HZ = 1024, 2.4e9   # 256 CUs x 4 SIMDs; peak engine clock (one wave64 VALU per 4 cycles)
-FLOP_PER_SPHERE_TEST = 17
+PEAK_TF = {"f32": 157.3, "f64": 78.6}   # MI355X vector peaks (MI355X_MICROARCH.md chip table; AMD spec fp64)
+FLOP_PER_SPHERE_TEST = 17   # the reference's mandatory test per (segment, sphere)
 
 
 def parse():
@@ -43,19 +46,46 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C")
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--other-precision", type=int, default=1, help="also time the other precision (0 = skip)")
     ap.add_argument("--seed", type=lambda s: int(s, 0), default=0x5EED0001)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = all cores of this process")
-    ap.add_argument("--traffic", default=os.path.join(REPO, "profiles", "traffic.json"))
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc.json"))
     ap.add_argument("--max-spheres", type=int, default=0, help="experiment: truncate the scene (not a bench line)")
     return ap.parse_args()
 
 
-def cpu_baseline(flat, cam, depth, spp, seed, budget_s, threads):
+def cpu_share():
+    """Cores this process may run on: the affinity set, capped by the cgroup v2 CPU quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    threads = aff if quota is None else max(1, min(aff, int(quota)))
+    return threads, {"nproc": os.cpu_count(), "affinity": aff, "cgroup_cpu_quota": quota, "cpu_model": model}
+
+
+def cpu_baseline(flat, cam, depth, spp, seed, budget_s, threads, host):
     """Oracle (CPU restatement, f64) on a strided pixel sample; grows the sample until ~budget_s."""
     import numpy as np
     sys.path.insert(0, os.path.join(REPO, "tests"))
-    from oracle_bind import oracle_render
+    import oracle_bind
+    lib_path = oracle_bind.build_native()
+    build = "-O3 -march=native" if lib_path else "-O3 -march=x86-64-v3 (native build failed)"
     W, H = cam.image_width, cam.image_height
     n_all = W * H
     order = (np.arange(n_all, dtype=np.int64) * 7919) % n_all   # 7919 prime, coprime with W*H
@@ -65,21 +95,25 @@ def cpu_baseline(flat, cam, depth, spp, seed, budget_s, threads):
         if len(px) == 0:
             break
         t0 = time.perf_counter()
-        _, _, s, rc = oracle_render(flat, cam, depth, spp, seed, 0, pixels=px, precision="f64", threads=threads)
+        _, _, s, rc = oracle_bind.oracle_render(flat, cam, depth, spp, seed, 0, pixels=px, precision="f64",
+                                                threads=threads, lib_path=lib_path)
         t_used += time.perf_counter() - t0
         done += len(px)
         segs += s
         batch = int(1.1 * max(0.0, budget_s - t_used) / (t_used / done))
         if t_used >= 0.95 * budget_s:
             break
-    return {
+    out = {
         "value": done * spp / t_used / 1e6,
         "unit": "Msamples/s",
         "cores": threads,
         "kind": "port",
         "sample": f"{done} of {n_all} pixels (stride-7919 permutation) x {spp} spp, f64, {t_used:.1f} s",
+        "build": build,
         "ray_segments_per_sample": segs / (done * spp),
     }
+    out.update(host)
+    return out
 
 
 def main():
@@ -104,6 +138,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group(backend)
+    dist_on = dist.is_initialized()
+    world_init = dist.get_world_size() if dist_on else 1
 
     import rt_mi355x as rt
     from rt_mi355x import abi
@@ -116,7 +152,6 @@ def main():
         n_sph = len(scene.objects)
     flat = scene.flatten()
     cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
-    flags = abi.RT_FLAG_F32 if args.precision == "f32" else 0
 
     ctx = ctypes.c_void_p()
     abi.check(lib, lib.rt_context_create(device, ctypes.byref(ctx)))
@@ -129,10 +164,15 @@ def main():
     image = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
-    def step():
+    def step(flags, ev=None):
+        if ev:
+            ev[0].record(stream)
         abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tile),
                                            ctypes.c_void_p(shard.data_ptr()), None, sptr))
+        if ev:
+            ev[1].record(stream)
         if world > 1:
             if backend == "nccl":   # RCCL over xGMI, device buffers
                 dist.gather(shard, gathered, dst=0)
@@ -142,71 +182,112 @@ def main():
                 if rank == 0:
                     for g, h in zip(gathered, host):
                         g.copy_(h)
+            if ev:
+                ev[2].record(stream)
             if rank == 0:
                 parallel.assemble_rows(gathered, H, world, image)
-        elif rank == 0:
-            image.copy_(shard[:H])
+        else:
+            if ev:
+                ev[2].record(stream)
+            if rank == 0:
+                image.copy_(shard[:H])
+        if ev:
+            ev[3].record(stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    st = abi.RtStats()
-    abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(st)), allow=(abi.RT_ERR_RANGE,))
+    def leg(precision):
+        """Warm-up, then exactly args.steps timed steps between barriers; max over ranks."""
+        flags = abi.RT_FLAG_F32 if precision == "f32" else 0
+        for _ in range(args.warmup):
+            step(flags)
+        torch.cuda.synchronize()
+        abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(abi.RtStats())), allow=(abi.RT_ERR_RANGE,))
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            step(flags, evs[k])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        st = abi.RtStats()
+        rc = abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(st)), allow=(abi.RT_ERR_RANGE,))
+        phase = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / args.steps for i in range(3)]   # ms per step
+        px_s = tile.row_count * W / (phase[0] / 1e3) if phase[0] > 0 else 0.0   # this shard's px/s (renderer.rs:339)
+        mine = [elapsed, phase[0], phase[1], phase[2], float(st.ray_segments), px_s]
+        if world > 1:
+            t = torch.tensor(mine, dtype=torch.float64, device=red_dev)
+            allr = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(allr, t)
+            per_rank = [a.cpu().tolist() for a in allr]
+        else:
+            per_rank = [mine]
+        return st, rc, per_rank
 
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    def summarize(precision, st, rc, per_rank):
+        elapsed = max(r[0] for r in per_rank)
+        samples = W * H * spp * args.steps
+        launch_s = per_rank[rank][1] / 1e3   # this rank's average launch (render) duration
+        f32, f64 = abi.executed_flop(st, precision)
+        f32, f64 = f32 / args.steps, f64 / args.steps   # per launch
+        t_peak = f32 / (PEAK_TF["f32"] * 1e12) + f64 / (PEAK_TF["f64"] * 1e12)   # seconds at peak
+        segs_launch = st.ray_segments / args.steps
+        bf = FLOP_PER_SPHERE_TEST * n_sph * segs_launch
+        return {
+            "value": samples / elapsed / 1e6,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "launch_ms": launch_s * 1e3,
+            "roofline": {
+                "bound": "valu",
+                "achieved": (f32 + f64) / launch_s / 1e12,
+                "peak": (f32 + f64) / t_peak / 1e12 if t_peak > 0 else PEAK_TF["f32"],
+                "unit": "TFLOP/s",
+                "frac": t_peak / launch_s,
+                "executed_flop_per_launch": {"fp32": f32, "fp64": f64},
+                "work_per_launch": {k: getattr(st, k) / args.steps for k in
+                                    ("box_groups", "filter_groups", "exact_tests", "cone_tests", "camera_exact_tests")},
+                "brute_force_equiv": {"flop_per_launch": bf, "tflops": bf / launch_s / 1e12,
+                                      "x_fp32_peak": bf / launch_s / 1e12 / PEAK_TF["f32"]},
+            },
+            "ray_segments_per_sample": st.ray_segments / (tile.row_count * W * spp * args.steps),
+            "lane_utilisation": st.ray_segments / max(1, st.lane_slots),
+            "bounces_per_pixel": st.bounce_iters / max(1, st.pixels),
+            "range_error": rc == abi.RT_ERR_RANGE,
+            "per_rank": per_rank,
+        }
 
-    st = abi.RtStats()
-    rc = abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(st)), allow=(abi.RT_ERR_RANGE,))
-    segs = st.ray_segments
-    kernel_ms = st.kernel_ms
-
-    red_dev = "cuda" if backend == "nccl" else "cpu"
-    stats = torch.tensor([elapsed, float(segs), kernel_ms], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        t_max = stats[0].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        seg_sum = stats[1].clone()
-        dist.all_reduce(seg_sum, op=dist.ReduceOp.SUM)
-        elapsed = float(t_max.item())
-        segs_total = int(seg_sum.item())
-    else:
-        segs_total = int(segs)
+    head = summarize(args.precision, *leg(args.precision))
+    if rank == 0 and os.environ.get("RT_BENCH_SAVE"):   # the headline precision's frame
+        np.save(os.environ["RT_BENCH_SAVE"], image.cpu().numpy())
+    other = None
+    if args.other_precision:
+        op = "f64" if args.precision == "f32" else "f32"
+        other = (op, summarize(op, *leg(op)))
 
     if rank == 0:
-        samples = W * H * spp * args.steps
-        value = samples / elapsed / 1e6
-        # roofline on rank 0's own kernel: its algorithmic FLOPs / its average launch duration
-        launch_s = (kernel_ms / 1e3) / args.steps
-        flop_launch = FLOP_PER_SPHERE_TEST * n_sph * (segs / args.steps)
-        achieved = flop_launch / launch_s / 1e12
-        peak = FP32_VALU_PEAK_TF
-        traffic, valu_insts = None, None
+        pmc = {}
         try:
-            with open(args.traffic) as f:
-                tr = json.load(f)
-            key = f"{args.config}:{args.precision}:{world}"
-            traffic = tr.get(key, {}).get("hbm_bytes_per_launch")
-            valu_insts = tr.get(key, {}).get("valu_insts_per_launch")
+            with open(args.pmc) as f:
+                pmc = json.load(f).get(f"{args.config}:{args.precision}:{world}", {})
         except (OSError, ValueError):
             pass
+        rl = head["roofline"]
+        rl["traffic"] = pmc.get("hbm_bytes_per_launch")
+        rl["algorithmic_bytes"] = tile.row_count * W * 3 + flat.n_spheres * 20   # RGB8 out + the scene (SoA)
+        rl["traffic_over_algorithmic"] = (rl["traffic"] / rl["algorithmic_bytes"]) if rl["traffic"] else None
+        rl["valu_busy"] = pmc.get("valu_busy")
+        rl["pmc_source"] = ({"file": os.path.relpath(args.pmc, REPO), "commit": pmc.get("commit"),
+                             "launch_ms": pmc.get("launch_ms")} if pmc else None)
         line = {
             "metric": "Msamples/s (pixels×spp/s), 1920×1080·512spp·500 spheres; 1/2/4/8 GPU",
-            "value": round(value, 3),
+            "value": round(head["value"], 3),
             "unit": "Msamples/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "ms_per_step": round(head["ms_per_step"], 3),
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -220,33 +301,35 @@ def main():
                                + ((" + RCCL gather" if backend == "nccl" else f" + {backend} gather (rehearsal)")
                                   if world > 1 else ""),
             },
-            "roofline": {
-                "bound": "valu",
-                "achieved": round(achieved, 3),
-                "peak": peak,
-                "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4),
-                "traffic": traffic,
-                "flop_per_launch": flop_launch,
-                "launch_ms": round(launch_s * 1e3, 3),
-                "valu_issue_frac": (round(valu_insts * 4 / (N_SIMD * launch_s * CLOCK_HZ), 4)
-                                    if valu_insts else None),
-            },
-            "ray_segments_per_sample": round(segs_total / samples, 5),
-            "lane_utilisation": round(st.ray_segments / max(1, st.lane_slots), 4),
-            "bounces_per_pixel": round(st.bounce_iters / max(1, st.pixels), 3),
-            "range_error": rc == abi.RT_ERR_RANGE,
+            "roofline": rl,
+            "launch_ms": round(head["launch_ms"], 3),
+            "ray_segments_per_sample": round(head["ray_segments_per_sample"], 5),
+            "lane_utilisation": round(head["lane_utilisation"], 4),
+            "bounces_per_pixel": round(head["bounces_per_pixel"], 3),
+            "range_error": head["range_error"],
+        }
+        if other:
+            op, o = other
+            line[op] = {"value": round(o["value"], 3), "ms_per_step": round(o["ms_per_step"], 3),
+                        "launch_ms": round(o["launch_ms"], 3), "roofline_frac": round(o["roofline"]["frac"], 4),
+                        "achieved_tflops": round(o["roofline"]["achieved"], 3),
+                        "brute_force_equiv_tflops": round(o["roofline"]["brute_force_equiv"]["tflops"], 3),
+                        "range_error": o["range_error"]}
+        line["dist"] = {
+            "backend": (backend if dist_on else None), "world_size_initialised": world_init,
+            "rccl_version": (".".join(map(str, torch.cuda.nccl.version())) if dist_on and backend == "nccl" else None),
+            "per_rank": [{"rank": r, "wall_s": round(p[0], 4), "render_ms": round(p[1], 3), "gather_ms": round(p[2], 3),
+                          "assemble_ms": round(p[3], 3), "ray_segments": int(p[4]), "px_per_s": round(p[5], 1)}
+                         for r, p in enumerate(head["per_rank"])],
         }
         if world == 1 and args.cpu_seconds > 0:
-            threads = args.cpu_threads or min(16, len(os.sched_getaffinity(0)))
-            line["cpu_baseline"] = cpu_baseline(flat, cam, depth, spp, args.seed, args.cpu_seconds, threads)
+            threads, host = cpu_share()
+            threads = args.cpu_threads or threads
+            line["cpu_baseline"] = cpu_baseline(flat, cam, depth, spp, args.seed, args.cpu_seconds, threads, host)
         else:
             line["cpu_baseline"] = None
         print(json.dumps(line), flush=True)
 
-    if rank == 0 and os.environ.get("RT_BENCH_SAVE"):
-        import numpy as np
-        np.save(os.environ["RT_BENCH_SAVE"], image.cpu().numpy())
     lib.rt_context_destroy(ctx)
     if dist.is_initialized():
         dist.destroy_process_group()

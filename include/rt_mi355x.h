@@ -87,6 +87,16 @@ typedef struct rt_stats {
     uint64_t lane_slots;     /* SIMD lanes issued for those traces (64 per wave-bounce);
                                 ray_segments / lane_slots = lane utilisation */
     uint64_t bounce_iters;   /* bounce-loop iterations executed, summed over pixels */
+    /* Executed work of the culls and exact tests, in wave-level tests (each runs all 64 lanes of a
+     * wave); DESIGN.md §5 turns them into executed FLOP for the roofline:
+     *   box_groups          general sweep, 4 boxes each: 18 v_pk_fma_f32 = 72 fp32 FLOP per lane
+     *   filter_groups       general sweep, 4 spheres each: 14 v_pk_fma_f32 = 56 fp32 FLOP per lane
+     *   exact_tests         general sweep, one sphere each through Sphere::hit_packed's test
+     *                       (objects.rs:252-257): 17 FLOP per lane in the render's precision
+     *   cone_tests          camera sweep, 64 cone records each: 23 fp32 FLOP per lane
+     *   camera_exact_tests  camera sweep, one sphere each from the camera-origin table: 8 FLOP per
+     *                       lane in the render's precision */
+    uint64_t box_groups, filter_groups, exact_tests, cone_tests, camera_exact_tests;
 } rt_stats;
 
 /* ---- flags ---- */
@@ -143,8 +153,10 @@ int rt_render_async(rt_context* ctx, const rt_camera* camera, uint32_t max_bounc
                     void* d_linear, void* stream);
 /* RenderStat (renderer.rs:11-34) for the renders since the last call.
  * Synchronise `stream` (NULL = null stream), then report and reset the counters accumulated by the renders
- * enqueued since the last call (ray_segments, error flag).  kernel_ms = device time between
- * the first and last enqueued render (HIP events on that stream). */
+ * enqueued since the last call (ray_segments, work counters, error flag).  kernel_ms = device time
+ * between the first and last enqueued render (HIP events on that stream); pixels_per_second =
+ * pixels / kernel_ms (the per-shard px/s the reference prints per tile, renderer.rs:339);
+ * seconds = 0 (rt_render fills in its wall time). */
 int rt_context_collect(rt_context* ctx, void* stream, rt_stats* stats);
 /* Device memory helpers (so hosts without a HIP toolchain can drive the async API); no reference
  * counterpart (the reference has no device memory). */

@@ -136,18 +136,34 @@ template <typename T> struct KParams {
 
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
-constexpr int kWavesF32 = 5;   // default min-waves-per-SIMD targets (measured sweep)
-constexpr int kWavesF64 = 4;
-// fp32 launches whose samples per resident wave at W6 reach this run at W6: +0.9 % on a whole frame of
-// config C, but the smaller per-wave share of an 8-way shard leaves a tail (5.62 -> 6.14 ms), so W5 there.
-constexpr int kWavesF32Big = 6;
-constexpr uint64_t kBigWaveSamples = 32768;
+constexpr int kWavesF32 = 5;   // default min-waves-per-SIMD targets (measured sweep);
+constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
 constexpr double kExactRatio = 8.0;  // spheres with |c|_1 + r > kExactRatio x the median are "always exact"
 
-// Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..6.
+// Executed-work counters (product build): per wave, the wave-level tests the culls and
+// exact tests actually run, one LDS add per sweep or camera batch, flushed to shard slots
+// kWorkSlot.. at the end.  The host turns them into executed FLOP (rt_work_stats).
+enum WorkCounter : uint32_t {
+    kWBox = 0,      // general sweep: box groups tested (4 boxes, 18 v_pk_fma_f32)
+    kWFilt = 1,     // general sweep: filter groups tested (4 spheres, 14 v_pk_fma_f32)
+    kWExact = 2,    // general sweep: spheres through the reference's exact test (17 FLOP in T each)
+    kWCone = 3,     // camera sweep: cone tests (64 records per wave test, 23 fp32 FLOP)
+    kWCExact = 4,   // camera sweep: exact tests from the camera-origin table (8 FLOP in T each)
+    kNWork = 5,
+};
+constexpr int kWorkSlot = 11;   // shard slots 11..15 (kstats uses 3..10)
+static_assert(kWorkSlot + kNWork <= kSegStride, "work counters past the shard's line");
+__shared__ uint32_t g_work[4][kNWork];
+// Add wave-uniform counts from the first active lane (the caller may be inside a divergent branch).
+__device__ __forceinline__ void work_add(uint32_t i, uint32_t n) {
+    const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
+    if ((threadIdx.x & 63u) == first) atomicAdd(&g_work[threadIdx.x >> 6][i], n);
+}
+
+// Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..10.
 #ifdef RT_KSTATS
 __shared__ unsigned long long g_kst[4][8];
 __device__ __forceinline__ void kstat(uint32_t i, uint32_t n = 1) {
@@ -182,8 +198,8 @@ template <typename T> __device__ __forceinline__ cptr<KParams<T>> cold_args_afte
 // x / W for the camera's pixel coordinate (ray_tracing.rs:78-79), W the image width or height.
 // fp32: RN_f(RN_d(x * RN_d(1/W))) == RN_f(x / W).  The double product is within 2^-52 relative of
 // x / W; a quotient of a float by an integer W < 2^20 that is not a float midpoint lies at least
-// ~2^-44 relative from every midpoint, and it is never one (an odd 25-bit mantissa times W has more
-// than 24 significant bits).  3 ops instead of the ~10 of a correctly rounded fp32 divide.  The
+// 2^-25 / W (>= 2^-45) relative from every midpoint, and it is never one (an odd 25-bit mantissa
+// times W has more than 24 significant bits).  3 ops instead of the ~10 of a correctly rounded fp32 divide.  The
 // host sets r = 0 (plain division) for larger images; fp64 always divides.
 template <typename T> __device__ __forceinline__ T div_dim(T x, uint32_t W, double r) {
     if constexpr (sizeof(T) == 4) {
@@ -659,9 +675,15 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // walks the set clusters' groups with the per-sphere filter and, where it passes, the exact
         // test.  The phases never hold both SGPR pipelines at once (no SGPR spills).
         const uint32_t nxg = qa.n_xg, ntop = qa.n_top;
+        // executed-work counts of this sweep (wave-uniform; work_add below)
+        uint32_t n_box = 0, n_filt = 0, n_exact = 0;
         // the always-exact groups; fp32 skips a pair of dummies at the end (the ground sphere's group
         // at config C: ground + 3 dummies); in fp64 the variable pair mask costs VGPR spills at W4
-        for (uint32_t g = 0; g < nxg; ++g) exact4(g, sizeof(T) == 4 && 4u * g + 2u >= qa.n_xs ? 1u : 3u);
+        for (uint32_t g = 0; g < nxg; ++g) {
+            const uint32_t pr = sizeof(T) == 4 && 4u * g + 2u >= qa.n_xs ? 1u : 3u;
+            n_exact += pr == 3u ? 4u : 2u;
+            exact4(g, pr);
+        }
         // Three levels: super boxes (4 clusters each, 4 per group) per chunk of 32 supers, then the
         // passing supers' cluster boxes (one group each), then the passing clusters' sphere groups.
         cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 32);
@@ -669,6 +691,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         const uint32_t nsg = (ntop + 3u) / 4u;   // super groups (ntop supers, one per cluster top group)
         for (uint32_t t0 = 0; t0 < nsg; t0 += 8u) {
             uint32_t smask = 0;
+            n_box += min(8u, nsg - t0);
             box_loop(fs + kBoxFloats * t0, min(8u, nsg - t0), [&](const BoxGroup& cur, uint32_t t) {
                 KSTAT(5);
                 smask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
@@ -680,14 +703,18 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 // NaN) passes them, and they have no cluster boxes behind them
                 if (sup >= ntop) break;
                 KSTAT(5);
+                ++n_box;
                 uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
                 while (mask != 0u) {
                     const uint32_t g0 = nxg + 4u * (4u * sup + (uint32_t)__builtin_ctz(mask));
                     mask &= mask - 1u;
                     KSTAT(4);
+                    n_filt += 4u;
                     sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                         uint32_t s0, s1;
-                        if (is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) {
+                        // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
+                        // rejects them as well (the filter passes every sphere the reference can hit).
+                        if (__ballot(is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) != 0ull) {
                             // only the sphere pairs some lane passes (one compare each, taken groups only)
                             uint32_t pairs = 3u;
 #ifndef RT_EXP_PAIRS_F64
@@ -695,12 +722,16 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 #endif
                                 pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
                                         (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
+                            n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
                             exact4(g0 + g, pairs);
                         }
                     });
                 }
             }
         }
+        work_add(kWBox, n_box);
+        work_add(kWFilt, n_filt);
+        work_add(kWExact, n_exact);
 #endif
     }
     t_out = best_t;
@@ -811,9 +842,12 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
                 hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
         }
     };
+    uint32_t n_cone = 0, n_cx = 0;   // executed-work counts (work_add below)
     // 1. the always-exact spheres (build_layout's leading slots), lanes as spheres
     for (uint32_t base = 0; base < nx; base += 64u) {
+        ++n_cone;
         unsigned long long m = __ballot(base + lane < nx && cone(base == 0 ? xw0 : cs[base + lane]));
+        n_cx += (uint32_t)__popcll(m);
         while (m != 0ull) {
             const uint32_t s = base + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
@@ -823,8 +857,10 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
     // to 4 passing clusters per pass, 16 lanes each
     for (uint32_t cb = 0; cb < ncl; cb += 64u) {
+        ++n_cone;
         unsigned long long M = __ballot(cone(cb == 0 ? kw0 : cc[cb + lane]));   // padded to whole 64s
         while (M != 0ull) {
+            ++n_cone;
             uint32_t k[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {   // empty quarters take the padding cluster ncl (all dummies)
@@ -834,6 +870,7 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
             const uint32_t qd = lane >> 4;
             const uint32_t kl = qd == 0 ? k[0] : qd == 1 ? k[1] : qd == 2 ? k[2] : k[3];
             unsigned long long m = __ballot(cone(cs[nx + 16u * kl + (lane & 15u)]));
+            n_cx += (uint32_t)__popcll(m);
             while (m != 0ull) {
                 const uint32_t b = (uint32_t)__builtin_ctzll(m);
                 m &= m - 1ull;
@@ -842,6 +879,8 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
             }
         }
     }
+    work_add(kWCone, n_cone);
+    work_add(kWCExact, n_cx);
     t_out = best_t;
     return best;
 }
@@ -1416,6 +1455,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
+    if (lane < kNWork) g_work[wave][lane] = 0u;
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
@@ -1710,6 +1750,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         atomicAdd(cc + 0, wcount[wave][0]);
         atomicAdd(cc + 1, wcount[wave][1]);
         atomicAdd(cc + 2, wcount[wave][2]);
+        for (uint32_t i = 0; i < kNWork; ++i) atomicAdd(cc + kWorkSlot + i, (unsigned long long)g_work[wave][i]);
 #ifdef RT_KSTATS
         for (int i = 0; i < 8; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);
 #endif
@@ -2275,7 +2316,9 @@ static void (*pick_kernel(uint32_t flags, int W))(KParams<T>) {
     if (flags & RT_FLAG_MODE_VECTORIZED)
         return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
     if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
-    if (!CAMQ) return trace_paths<T, WM, false, kModeV2, false>;
+    if (!CAMQ)
+        return W >= 6 ? trace_paths<T, 6, false, kModeV2, false> : W >= 5 ? trace_paths<T, 5, false, kModeV2, false>
+                                                                  : trace_paths<T, 4, false, kModeV2, false>;
     return W >= 8 ? trace_paths<T, 8, false, kModeV2, true> : W >= 6 ? trace_paths<T, 6, false, kModeV2, true>
          : W >= 5 ? trace_paths<T, 5, false, kModeV2, true> : trace_paths<T, 4, false, kModeV2, true>;
 }
@@ -2353,12 +2396,11 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_items = rg.row_count * rg.col_count;
 
     // Persistent grid: as many 4-wave workgroups as stay resident, never more waves than pixels.
-    // Minimum waves per SIMD the register allocation targets (RT_WAVES overrides; experiments).
-    static const int waves_env = [] { const char* e = getenv("RT_WAVES"); return e ? atoi(e) : 0; }();
-    const uint64_t big_samples = (uint64_t)c->n_cu * 4u * kWavesF32Big * kBigWaveSamples;
-    const int W = waves_env ? waves_env
-                : sizeof(T) == 8 ? kWavesF64
-                : (uint64_t)rg.row_count * rg.col_count * spp >= big_samples ? kWavesF32Big : kWavesF32;
+    // Minimum waves per SIMD the register allocation targets.  RT_WAVES (4, 5, 6; read at every
+    // launch, so one process can compare them) overrides it for the live-path kernels (pinhole and
+    // defocus cameras); the ROOT2 and semantics-mode kernels always run at kWavesModes.
+    const char* waves_env = getenv("RT_WAVES");
+    const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : sizeof(T) == 8 ? kWavesF64 : kWavesF32;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
     void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W) : pick_kernel<T, false>(flags, W);
@@ -2466,7 +2508,7 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
     HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
     HIPCHK(hipMemset(c->err, 0, 16));
-    uint64_t total = 0, slots = 0, iters = 0, kst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t total = 0, slots = 0, iters = 0, kst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, work[kNWork] = {};
     for (int i = 0; i < kSegShards; ++i)
         for (int j = 0; j < 8; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
     if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
@@ -2479,6 +2521,7 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
         total += segs[(size_t)i * kSegStride];
         slots += segs[(size_t)i * kSegStride + 1];
         iters += segs[(size_t)i * kSegStride + 2];
+        for (uint32_t j = 0; j < kNWork; ++j) work[j] += segs[(size_t)i * kSegStride + kWorkSlot + j];
     }
     if (out) {
         memset(out, 0, sizeof(*out));
@@ -2488,6 +2531,12 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
         out->ray_segments = total;
         out->lane_slots = slots;
         out->bounce_iters = iters;
+        out->pixels_per_second = ms > 0.f ? (double)c->pixels / ((double)ms * 1e-3) : 0.0;
+        out->box_groups = work[kWBox];
+        out->filter_groups = work[kWFilt];
+        out->exact_tests = work[kWExact];
+        out->cone_tests = work[kWCone];
+        out->camera_exact_tests = work[kWCExact];
     }
     c->have_first = false;
     c->pixels = c->samples = 0;

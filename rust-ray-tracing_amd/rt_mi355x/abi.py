@@ -62,7 +62,24 @@ class RtStats(ctypes.Structure):
         ("ray_segments", u64),
         ("lane_slots", u64),
         ("bounce_iters", u64),
+        ("box_groups", u64),
+        ("filter_groups", u64),
+        ("exact_tests", u64),
+        ("cone_tests", u64),
+        ("camera_exact_tests", u64),
     ]
+
+
+# Executed FLOP per lane of one wave-level test (include/rt_mi355x.h); x 64 lanes.
+WORK_FLOP_F32 = {"box_groups": 72, "filter_groups": 56, "cone_tests": 23}
+WORK_FLOP_T = {"exact_tests": 17, "camera_exact_tests": 8}   # in the render's precision
+
+
+def executed_flop(st, precision):
+    """(fp32 FLOP, fp64 FLOP) the culls and exact tests executed (64 lanes per wave-level test)."""
+    f32 = sum(64 * f * getattr(st, k) for k, f in WORK_FLOP_F32.items())
+    ft = sum(64 * f * getattr(st, k) for k, f in WORK_FLOP_T.items())
+    return (f32 + ft, 0) if precision == "f32" else (f32, ft)
 
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

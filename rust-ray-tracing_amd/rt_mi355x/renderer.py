@@ -66,7 +66,7 @@ class GpuRenderer(Renderer):
                       | self.MODES[mode])
         self.ctx = ctypes.c_void_p()
         abi.check(self.lib, self.lib.rt_context_create(device, ctypes.byref(self.ctx)))
-        self._scene_key = None
+        self._scene_flat = None   # the FlatScene last uploaded (held, so its identity cannot be reused)
 
     def close(self):
         if self.ctx:
@@ -81,12 +81,14 @@ class GpuRenderer(Renderer):
 
     def set_scene(self, flat):
         abi.check(self.lib, self.lib.rt_context_set_scene(self.ctx, ctypes.byref(flat.abi)))
-        self._scene_key = id(flat)
+        # A strong reference, compared with `is`: an id() key could match a new FlatScene that CPython
+        # allocated at a freed one's address, and the render would silently use the old spheres.
+        self._scene_flat = flat
 
     def render_flat(self, max_bounces, spp, flat, cam, tile_range=None, want_linear=False):
         """Render with a FlatScene / RtCamera; returns (rgb [n,3] u8, linear [n,3] f64 | None, RtStats, rc)."""
         lib = self.lib
-        if self._scene_key != id(flat):
+        if self._scene_flat is not flat:
             self.set_scene(flat)
         if tile_range is None:
             tr = abi.RtTileRange(0, 1, cam.image_height, 0, cam.image_width)

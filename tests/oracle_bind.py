@@ -12,16 +12,24 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(REPO, "oracle")
 ORACLE_PATH = os.path.join(ORACLE_DIR, "build", "liboracle.so")
 
-_lib = None
+NATIVE_PATH = os.path.join(ORACLE_DIR, "build", "native", "liboracle.so")
+
+_libs = {}
 
 
-def load_oracle():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(ORACLE_PATH):
+def build_native():
+    """Build the -march=native oracle on this host (bench.py's CPU baseline); returns its path or None."""
+    r = subprocess.run(["make", "-C", ORACLE_DIR, "native"], capture_output=True, text=True)
+    return NATIVE_PATH if r.returncode == 0 and os.path.exists(NATIVE_PATH) else None
+
+
+def load_oracle(path=None):
+    path = path or ORACLE_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         subprocess.run(["make", "-C", ORACLE_DIR], check=True, capture_output=True)
-    lib = ctypes.CDLL(ORACLE_PATH)
+    lib = ctypes.CDLL(path)
     vp, u32, u64, f64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_double
     for name in ("oracle_render_f64", "oracle_render_f32"):
         fn = getattr(lib, name)
@@ -33,14 +41,15 @@ def load_oracle():
     lib.oracle_sincos2pi_f64.argtypes = [f64, ctypes.POINTER(f64), ctypes.POINTER(f64)]
     lib.oracle_to_u8.argtypes = [ctypes.POINTER(f64), ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int)]
     lib.oracle_get_ray_f64.argtypes = [vp, u32, u32, u32, u64, ctypes.POINTER(f64), ctypes.POINTER(f64)]
-    _lib = lib
+    _libs[path] = lib
     return lib
 
 
-def oracle_render(flat, cam, max_bounces, spp, seed, flags=0, pixels=None, precision="f64", threads=None):
+def oracle_render(flat, cam, max_bounces, spp, seed, flags=0, pixels=None, precision="f64", threads=None,
+                  lib_path=None):
     """Run the CPU restatement.  flat: rt_mi355x.FlatScene; cam: abi.RtCamera.
     Returns (rgb [n,3] u8, linear [n,3] f64, segments, rc)."""
-    lib = load_oracle()
+    lib = load_oracle(lib_path)
     if threads is None:
         threads = min(16, os.cpu_count() or 1)
     if pixels is None:
