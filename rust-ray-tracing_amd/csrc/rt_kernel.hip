@@ -112,7 +112,8 @@ template <typename T> struct KParams {
     uint32_t n_items;
     char* scratch;             // per-wave scratch regions
     size_t scratch_stride;
-    uint32_t vbytes, sbytes;   // trace_paths: value-array bytes, per-slot record bytes (PScratch)
+    uint32_t vbytes, sbytes;   // trace_paths: position-map bytes, per-slot record bytes (PScratch)
+    uint32_t swide;            // PScratch::wide
     const T* camsph;           // camera-origin table {oc, c} in the sph layout (pinhole launches)
     const float* fsph;         // filter stream: fp32 groups of 4 {cx, cy, cz, r2f} (layout above)
     const float* camf;         // camera filter table: fp32 groups of 4 {ocx, ocy, ocz, sc} (build_cam_table)
@@ -1100,23 +1101,48 @@ enum Mode : int {
     kModeScalar = 2,   // render -> trace_rays (ray_tracing.rs:264-306) + Color::average
 };
 
-// Per-wave scratch of trace_paths: the position-indexed value array (3 x P) for the pixel being
-// reduced, then kSlots record regions {y[P], c[3][P], e[P]} indexed by sample.  In the V1 and
-// scalar modes c holds each sample's final value (colour x sky of its own escaping ray, or 0).
+// Per-wave scratch of trace_paths (HBM layout): the position map of the pixel being
+// reduced (P entries, u16 -- u32 past 65532 positions: the sample whose value position q holds at the
+// final read, all ones = none), then kSlots record regions indexed by sample: y[P] (T, the primary
+// ray's y), c[P] (3 T, AoS: one dwordx3 store per termination), e[P] (u8 -- u32 when depth > 254: the
+// termination bounce).  In the V1 and scalar modes c holds each sample's final value (colour x sky of
+// its own escaping ray, or 0).
+template <typename T> struct C3 { T x, y, z; };
 template <typename T> struct PScratch {
     char* base;        // wave-uniform
-    uint32_t P, vbytes, sbytes;
-    __device__ __forceinline__ T& v(uint32_t ch, uint32_t q) const {
-        return *(T*)(base + (ch * P + q) * (uint32_t)sizeof(T));
+    uint32_t P, vbytes, sbytes, wide;   // wide: bit 0 = u32 e, bit 1 = u32 map
+    static constexpr uint32_t kNone = 0xFFFFFFFFu;
+    __device__ __forceinline__ uint32_t map(uint32_t q) const {
+        if (wide & 2u) return *(const uint32_t*)(base + 4u * q);
+        const uint32_t m = *(const uint16_t*)(base + 2u * q);
+        return m == 0xFFFFu ? kNone : m;
+    }
+    __device__ __forceinline__ void set_map(uint32_t q, uint32_t smp) const {
+        if (wide & 2u) *(uint32_t*)(base + 4u * q) = smp;
+        else *(uint16_t*)(base + 2u * q) = (uint16_t)smp;
     }
     __device__ __forceinline__ T& y(uint32_t s, uint32_t i) const {
         return *(T*)(base + vbytes + s * sbytes + i * (uint32_t)sizeof(T));
     }
-    __device__ __forceinline__ T& c(uint32_t s, uint32_t ch, uint32_t i) const {
-        return *(T*)(base + vbytes + s * sbytes + ((1u + ch) * P + i) * (uint32_t)sizeof(T));
+    __device__ __forceinline__ C3<T>& c(uint32_t s, uint32_t i) const {
+        return *(C3<T>*)(base + vbytes + s * sbytes + (P + 3u * i) * (uint32_t)sizeof(T));
     }
-    __device__ __forceinline__ uint32_t& e(uint32_t s, uint32_t i) const {
-        return *(uint32_t*)(base + vbytes + s * sbytes + 4u * P * (uint32_t)sizeof(T) + i * 4u);
+    __device__ __forceinline__ void store_c(uint32_t s, uint32_t i, T x, T y, T z) const {
+        T* r = &c(s, i).x;
+        r[0] = x;
+        asm volatile("" ::: "memory");   // keep the three stores apart (no dwordx3 merge)
+        r[1] = y;
+        asm volatile("" ::: "memory");
+        r[2] = z;
+    }
+    __device__ __forceinline__ uint32_t e(uint32_t s, uint32_t i) const {
+        const char* b = base + vbytes + s * sbytes + 4u * P * (uint32_t)sizeof(T);
+        return (wide & 1u) ? *(const uint32_t*)(b + 4u * i) : (uint32_t) * (const uint8_t*)(b + i);
+    }
+    __device__ __forceinline__ void set_e(uint32_t s, uint32_t i, uint32_t v) const {
+        char* b = base + vbytes + s * sbytes + 4u * P * (uint32_t)sizeof(T);
+        if (wide & 1u) *(uint32_t*)(b + 4u * i) = v;
+        else *(uint8_t*)(b + i) = (uint8_t)v;
     }
 };
 // This wave's scratch view, re-derived from the kernel arguments where it is used (it is needed
@@ -1124,7 +1150,7 @@ template <typename T> struct PScratch {
 template <typename T> __device__ __forceinline__ PScratch<T> wave_scratch(uint32_t wave) {
     const auto& q = *cold_args<T>();
     const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + wave;
-    return PScratch<T>{q.scratch + (size_t)gw * q.scratch_stride, q.P, q.vbytes, q.sbytes};
+    return PScratch<T>{q.scratch + (size_t)gw * q.scratch_stride, q.P, q.vbytes, q.sbytes, q.swide};
 }
 
 // Wave-uniform issue state, parked in LDS between refills for the same reason.
@@ -1175,8 +1201,12 @@ __device__ __forceinline__ bool guided_block(uint32_t np, uint32_t T, uint32_t G
     return false;
 }
 
-__host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t tsz) { return (3u * P * tsz + 255u) & ~255u; }
-__host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz) { return (P * (4u * tsz + 4u) + 255u) & ~255u; }
+// PScratch sizes: the map (u16, u32 past 65532 positions), the records (e u8, u32 when depth > 254).
+__host__ __device__ inline uint32_t paths_wide(uint32_t P, uint32_t depth) { return (depth > 254u ? 1u : 0u) | (P > 65532u ? 2u : 0u); }
+__host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t wide) { return (P * ((wide & 2u) ? 4u : 2u) + 255u) & ~255u; }
+__host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz, uint32_t wide) {
+    return (P * (4u * tsz + ((wide & 1u) ? 4u : 1u)) + 255u) & ~255u;
+}
 
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
@@ -1197,65 +1227,62 @@ constexpr bool kSkipInit = true;   // timing experiment only: results are wrong
 constexpr bool kSkipInit = false;
 #endif
 template <typename T, int MODE>
-__device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item,
-                                                          uint32_t* hist) {
+__device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
+                                                 T (*stage)[64]) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
-    // Value init: positions [spp, P) are the missing lanes of a partial last chunk, disabled from
-    // the start (ray.rs:140-144), hit_sky at bounce 0 (ray_tracing.rs:421-424) with a zero
-    // primary direction -> sky(0); with depth 0 they stay white in buffer 0 (s_sel == 0).
-    // Positions [0, spp) start at 0 (a ray still enabled at the end contributes black).
+    constexpr uint32_t kNone = PScratch<T>::kNone;
+    // Map init: no position holds a terminated sample's value yet (survivors and never-written
+    // positions read 0; positions [spp, P), the missing lanes of a partial last chunk, get their
+    // fixed value in the final reduction).  Two u16 entries per u32 store.
     if (MODE == kModeV2 && !kSkipInit) {
-        const V3<T> s0 = sky(T(0.0));
-        const bool white0 = q.s_sel == 0u;
-        for (uint32_t qi = lane; qi < P; qi += 64u) {
-            T vr = 0, vg = 0, vb = 0;
-            if (qi >= spp) {
-                if (depth > 0) { vr = s0.x; vg = s0.y; vb = s0.z; }
-                else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
-            }
-            sc.v(0, qi) = vr; sc.v(1, qi) = vg; sc.v(2, qi) = vb;
+        if (sc.wide & 2u) {
+            for (uint32_t qi = lane; qi < P; qi += 64u) sc.set_map(qi, kNone);
+        } else {
+            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(sc.base + 2u * qi) = 0xFFFFFFFFu;
         }
     }
-    // Bounce iterations the reference runs: K = min(depth, max e + 1).
+    // Bounce iterations the reference runs: K = min(depth, max e + 1).  The same pass builds the
+    // histogram of the termination bounces below 64 (a sample terminated iff e < depth, and then
+    // e < K); it is only used when K <= 64.
     uint32_t K = 0;
+    const bool hist_on = MODE == kModeV2 && depth > 0u;
+    if (hist_on) {
+        hist[lane] = 0u;
+        __builtin_amdgcn_wave_barrier();
+    }
     if (depth > 0) {
         uint32_t me = 0;
-        for (uint32_t i = lane; i < spp; i += 64u) me = max(me, sc.e(s, i));
+        for (uint32_t b = 0; b < spp; b += 512u) {
+            uint32_t ev[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t i = b + 64u * u + lane;
+                ev[u] = i < spp ? sc.e(s, i) : 0u;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                me = max(me, ev[u]);
+                if (hist_on && b + 64u * u + lane < spp && ev[u] < depth && ev[u] < 64u) atomicAdd(&hist[ev[u]], 1u);
+            }
+        }
         K = min(depth, __builtin_amdgcn_readfirstlane(wave_max(me)) + 1u);
     }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
     wave_mem_sync();
     // One pass over the samples (K <= 64, the common case): lane k holds the per-bounce counts, so
     // every sample finds its positions from running counts and ballots over its own chunk of 64.
     // Sample s, terminated at bounce k = e_s < K, sat at pold = #{s' < s : e_s' >= k} during bounce
     // k and moves to pnew = n_{k+1} + #{s' < s : e_s' == k} in the sorted copy (n_k = #{e >= k});
-    // the retire rule then picks which of the two holds its value.  The same writes
-    // as the per-bounce loop below, which rescans the records once per bounce (one memory round trip
-    // per bounce and chunk; 12 % of config C's time).
+    // the retire rule then picks which of the two holds its value, and the position
+    // map records the sample there (the value itself is formed in the final reduction).
     bool replayed = false;
 #if !defined(RT_EXP_SKIP_REPLAY) && !defined(RT_EXP_OLD_REPLAY)
     if (MODE == kModeV2 && K > 0u && K <= 64u) {
         replayed = true;
-        hist[lane] = 0u;
-        __builtin_amdgcn_wave_barrier();
-        auto load_e = [&](uint32_t b, uint32_t (&ev)[8]) {   // e of samples b .. b+511 (8 chunks)
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t i = b + 64u * u + lane;
-                ev[u] = i < spp ? sc.e(s, i) : 0xFFFFFFFFu;
-            }
-        };
-        for (uint32_t b = 0; b < spp; b += 512u) {   // histogram of e (e < K)
-            uint32_t ev[8];
-            load_e(b, ev);
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (ev[u] < K) atomicAdd(&hist[ev[u]], 1u);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_wave_barrier();
         const uint32_t H = hist[lane];
         uint32_t pre = H;   // inclusive prefix sum over lanes: #{e <= lane}
 #pragma unroll
@@ -1267,14 +1294,16 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         uint32_t cge = 0, ceq = 0;   // lane k: samples of the earlier chunks with e >= k, e == k
         for (uint32_t b = 0; b < spp; b += 512u) {   // the samples in order, 64 at a time
             uint32_t ev[8];
-            load_e(b, ev);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t i = b + 64u * u + lane;
+                ev[u] = i < spp ? sc.e(s, i) : 0xFFFFFFFFu;
+            }
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 if (b + 64u * u >= spp) break;
                 const uint32_t i = b + 64u * u + lane, e = ev[u];
                 const bool in = i < spp, ret = e < K;
-                V3<T> c = mk(T(0), T(0), T(0));
-                if (ret) c = mk(sc.c(s, 0, i), sc.c(s, 1, i), sc.c(s, 2, i));
                 unsigned long long rem = __ballot(ret);
                 uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nk = 0, nn = 0;
 #ifdef RT_EXP_NO_POSLOOP   // timing experiment only: results are wrong
@@ -1309,15 +1338,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                     const bool U = q.s_sel == (ek & 1u);
                     const bool w_old = U && pold >= lo && pold < hi;
                     const bool w_new = !U || pnew < lo || pnew >= hi;
-                    if (w_old || w_new) {
-                        const uint32_t q1 = w_old ? pold : pnew;
-                        const V3<T> sk = sky(sc.y(s, q1));
-                        sc.v(0, q1) = c.x * sk.x; sc.v(1, q1) = c.y * sk.y; sc.v(2, q1) = c.z * sk.z;
-                    }
-                    if (w_old && w_new) {
-                        const V3<T> sk = sky(sc.y(s, pnew));
-                        sc.v(0, pnew) = c.x * sk.x; sc.v(1, pnew) = c.y * sk.y; sc.v(2, pnew) = c.z * sk.z;
-                    }
+                    if (w_old || w_new) sc.set_map(w_old ? pold : pnew, i);
+                    if (w_old && w_new) sc.set_map(pnew, i);
                 }
             }
         }
@@ -1355,20 +1377,11 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 if (eq) {
                     const uint32_t pold = cge + (uint32_t)__popcll(bge & lt_mask);
                     const uint32_t pnew = n_next + ceq + (uint32_t)__popcll(beq & lt_mask);
-                    const V3<T> c = mk(sc.c(s, 0, i), sc.c(s, 1, i), sc.c(s, 2, i));
                     const bool w_old = U && pold >= lo && pold < hi;
                     const bool w_new = !U || pnew < lo || pnew >= hi;
-                    // At most one write except when the old position retires now and the new one
-                    // later: one sky evaluation for the common case, a second only for that one.
-                    if (w_old || w_new) {
-                        const uint32_t q1 = w_old ? pold : pnew;
-                        const V3<T> sk = sky(sc.y(s, q1));
-                        sc.v(0, q1) = c.x * sk.x; sc.v(1, q1) = c.y * sk.y; sc.v(2, q1) = c.z * sk.z;
-                    }
-                    if (w_old && w_new) {
-                        const V3<T> sk = sky(sc.y(s, pnew));
-                        sc.v(0, pnew) = c.x * sk.x; sc.v(1, pnew) = c.y * sk.y; sc.v(2, pnew) = c.z * sk.z;
-                    }
+                    // At most one position except when the old one retires now and the new one later.
+                    if (w_old || w_new) sc.set_map(w_old ? pold : pnew, i);
+                    if (w_old && w_new) sc.set_map(pnew, i);
                 }
                 cge += (uint32_t)__popcll(bge);
                 ceq += (uint32_t)__popcll(beq);
@@ -1380,13 +1393,15 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     wave_mem_sync();
     // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
     // (ray_tracing.rs:499-502), then PackedColor::sum over the 4 lanes (color.rs:226-232).
+    // Position q's value (ray_tracing.rs:488-497): sample m = map[q] hit the sky -> c_m x sky(y_q),
+    // y_q the primary ray's y at slot q (quirk Q2); no sample -> 0 (still enabled: black); q >= spp
+    // (the missing lanes of a partial chunk: disabled from the start, ray.rs:140-144, hit_sky at
+    // bounce 0, ray_tracing.rs:421-424, zero direction) -> sky(0), or white at depth 0 when the final
+    // read is buffer 0.  All 64 lanes form the values of 64 positions at a time into LDS; lanes
+    // ch * 4 + l then add theirs in order.
     // V1: render_vectorized's packed_color + chunk (renderer.rs:120) is the same per-lane order,
     // over each sample's own value (+0 for the disabled lanes of a partial chunk: black x sky).
     // Scalar: Color::average (color.rs:66-85), one sequential sum over the samples.
-    auto val = [&](uint32_t ch, uint32_t pos) -> T {
-        if constexpr (MODE == kModeV2) return sc.v(ch, pos);
-        else return pos < spp ? sc.c(s, ch, pos) : T(0.0);
-    };
     T acc = T(0.0);
 #ifdef RT_EXP_SKIP_REDUCE   // timing experiment only: results are wrong
     if (false) {
@@ -1398,23 +1413,67 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             for (; i + 16 <= spp; i += 16) {
                 T v[16];
 #pragma unroll
-                for (int u = 0; u < 16; ++u) v[u] = sc.c(s, lane, i + u);
+                for (int u = 0; u < 16; ++u) {
+                    const T* cp = &sc.c(s, i + u).x;
+                    v[u] = cp[lane];
+                }
 #pragma unroll
                 for (int u = 0; u < 16; ++u) acc = acc + v[u];
             }
-            for (; i < spp; ++i) acc = acc + sc.c(s, lane, i);
+            for (; i < spp; ++i) acc = acc + (&sc.c(s, i).x)[lane];
         }
-    } else if (lane < 12u && !kSkipReduce) {
-        const uint32_t ch = lane >> 2, l = lane & 3u;
-        uint32_t j = 0;
-        for (; j + 16 <= C; j += 16) {
-            T v[16];
+    } else if (!kSkipReduce) {
+        const V3<T> s0 = sky(T(0.0));
+        const bool white0 = depth == 0u && q.s_sel == 0u;
+        // the 12 running sums live in LDS (the free histogram) between batches: a short live range
+        // keeps this loop from raising the kernel's register peak
+        T* accl = (T*)hist;
+        if (lane < 12u) accl[lane] = T(0.0);
+        for (uint32_t qb = 0; qb < P; qb += 64u) {
+            const uint32_t qq = qb + lane;
+            T vr = T(0.0), vg = T(0.0), vb = T(0.0);
+            if (qq < P) {
+                if (qq >= spp) {
+                    if (MODE == kModeV2) {
+                        if (depth > 0u) { vr = s0.x; vg = s0.y; vb = s0.z; }
+                        else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
+                    }
+                } else if constexpr (MODE == kModeV2) {
+                    const uint32_t m = sc.map(qq);
+                    if (m != kNone) {
+                        const C3<T> cm = sc.c(s, m);
+                        const V3<T> sk = sky(sc.y(s, qq));
+                        vr = cm.x * sk.x; vg = cm.y * sk.y; vb = cm.z * sk.z;
+                    }
+                } else {
+                    const C3<T> cm = sc.c(s, qq);
+                    vr = cm.x; vg = cm.y; vb = cm.z;
+                }
+            }
+            // transposed: lane (ch, l) finds its 16 values (positions qb + 4u + l) contiguous
+            const uint32_t si = 16u * (lane & 3u) + (lane >> 2);
+            stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 12u) {
+                const uint32_t nu = min(16u, (P - qb) / 4u);
+                const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
+                T a = accl[lane];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) v[u] = val(ch, 4 * (j + u) + l);
+                for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
+                    T v[4];
 #pragma unroll
-            for (int u = 0; u < 16; ++u) acc = acc + v[u];
+                    for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; ++u)
+                        if (u0 + u < nu) a = a + v[u];
+                }
+                accl[lane] = a;
+            }
+            __builtin_amdgcn_wave_barrier();
         }
-        for (; j < C; ++j) acc = acc + val(ch, 4 * j + l);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane < 12u) acc = accl[lane];
     }
     const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
             s3 = __shfl(acc, (int)((lane + 3) & 63u));
@@ -1447,6 +1506,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? kQCap : 1;
     __shared__ unsigned long long wcount[4][3];
     __shared__ uint32_t s_hist[4][64];
+    __shared__ __attribute__((aligned(16))) T s_stage[4][3][64];   // finish_pixel: 64 positions' values per wave
     __shared__ IssueState s_is[4];
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
     __shared__ uint32_t q_sid[QW][QN], q_pix[QW][QN];   // sid | slot << 29, pixel
@@ -1555,13 +1615,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                          const V3<T>& td) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
-            sc.e(t_slot, t_sid) = e;
+            sc.set_e(t_slot, t_sid, e);
             if (MODE == kModeV2) {
-                if (skyhit) { sc.c(t_slot, 0, t_sid) = tc.x; sc.c(t_slot, 1, t_sid) = tc.y; sc.c(t_slot, 2, t_sid) = tc.z; }
+                // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
+                // the copies into them raised the register peak (spills in the sphere sweeps)
+                if (skyhit) sc.store_c(t_slot, t_sid, tc.x, tc.y, tc.z);
             } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
                 V3<T> v = mk(T(0.0), T(0.0), T(0.0));
                 if (skyhit) { const V3<T> sk = sky(td.y); v = mk(tc.x * sk.x, tc.y * sk.y, tc.z * sk.z); }
-                sc.c(t_slot, 0, t_sid) = v.x; sc.c(t_slot, 1, t_sid) = v.y; sc.c(t_slot, 2, t_sid) = v.z;
+                sc.store_c(t_slot, t_sid, v.x, v.y, v.z);
             }
         }
         unsigned long long tm = __ballot(term);
@@ -1571,15 +1633,18 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const unsigned long long m = __ballot(term && t_slot == s);
             tm &= ~m;
             if (lane == s) slot_left -= (uint32_t)__popcll(m);
-            if (__builtin_amdgcn_readlane(slot_left, s) == 0u) {   // pixel complete
+            // pixel complete: once per spp samples -- marked unlikely, so the register allocator
+            // places any spill code here rather than in the sphere sweeps
+            if (__builtin_expect(__builtin_amdgcn_readlane(slot_left, s) == 0u, 0)) {
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
 #ifdef RT_EXP_DUP_FINISH   // timing experiment: finish_pixel twice (idempotent)
-                (void)finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave]);
+                (void)finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave],
+                                            s_stage[wave]);
                 wave_mem_sync();
 #endif
                 const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
-                                                         s_hist[wave]);
+                                                         s_hist[wave], s_stage[wave]);
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
@@ -2433,8 +2498,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         while (2u * G <= g) G *= 2u;
         p.blk_g = G;
     }
-    p.vbytes = paths_vbytes(p.P, sizeof(T));
-    p.sbytes = paths_sbytes(p.P, sizeof(T));
+    p.swide = paths_wide(p.P, depth);
+    p.vbytes = paths_vbytes(p.P, p.swide);
+    p.sbytes = paths_sbytes(p.P, sizeof(T), p.swide);
     p.scratch_stride = (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
     // Keep the scratch within a fixed budget: fewer resident waves for very large spp.
     const uint64_t kScratchBudget = 24ull << 30;

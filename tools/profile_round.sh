@@ -1,42 +1,36 @@
 #!/bin/bash
-# One GPU call that produces the judged artefacts for a round:
-#   <out>/bench.json            default bench line (N=1)
-#   <out>/ktrace/*stats.csv     rocprofv3 --kernel-trace --stats of the same bench command
-#   <out>/pmc_*                 FETCH_SIZE / WRITE_SIZE / SQ_INSTS_VALU passes (separate, counters only)
-#   profiles/traffic.json       HBM bytes per launch (FETCH doubled per MI355X_MICROARCH.md §HBM)
-# Usage (GPU box): bash tools/profile_round.sh gpurun_out/round [precision]
+# One GPU call that produces the judged profile artefacts of a round for one config/precision:
+#   <out>/pmc_{fetch,write,sq}/   rocprofv3 --pmc passes of bench.py (one counter group each, counters only)
+#   <out>/ubench_sq/              the same SQ pass over tools/bin/ubench_valu (VALU-saturating FMA chains:
+#                                 calibrates SQ_ACTIVE_INST_VALU's unit and the FLOPS counters' lane scale)
+#   <out>/bench.json              the bench line (after the PMC passes, so it reads this call's pmc.json)
+#   <out>/ktrace/*stats.csv       rocprofv3 --kernel-trace --stats of the same bench command
+#   <out>/pmc.json                HBM bytes / VALU busy / FLOP counters per launch (tools/pmc_round.py)
+# Usage (GPU box): bash tools/profile_round.sh <out> [precision] [config]
 set -u
 OUT=${1:-gpurun_out/round}
 PREC=${2:-f32}
+CFG=${3:-C}
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-STEPS=5
-for C in FETCH_SIZE WRITE_SIZE SQ_INSTS_VALU; do
-  timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex trace_ -d "$OUT/pmc_$C" -o run --output-format csv -- \
-      python3 bench.py --precision "$PREC" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/pmc_$C.log" 2>&1 || exit $?
-done
-python3 - "$OUT" "$PREC" <<'EOF'
-import csv, glob, json, os, sys
-out, prec = sys.argv[1], sys.argv[2]
-vals = {}
-for c in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU"):
-    rows = [r for f in glob.glob(f"{out}/pmc_{c}/**/*counter_collection.csv", recursive=True)
-            for r in csv.DictReader(open(f)) if "trace_" in r["Kernel_Name"]]
-    vals[c] = sum(float(r["Counter_Value"]) for r in rows) / max(1, len({r["Dispatch_Id"] for r in rows}))
-fetch_b, write_b = vals["FETCH_SIZE"] * 1024, vals["WRITE_SIZE"] * 1024
-rec = {"hbm_bytes_per_launch": 2 * fetch_b + write_b, "fetch_bytes_raw": fetch_b, "write_bytes": write_b,
-       "valu_insts_per_launch": vals["SQ_INSTS_VALU"],
-       "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 reports half of wide streaming reads); "
-               "per launch of config C on one GPU"}
-path = "profiles/traffic.json"
-db = json.load(open(path)) if os.path.exists(path) else {}
-db[f"C:{prec}:1"] = rec
-json.dump(db, open(path, "w"), indent=1)
-json.dump(rec, open(f"{out}/traffic.json", "w"), indent=1)
-print(json.dumps(rec))
-EOF
-# bench line and kernel trace after the traffic passes, so bench.json reads this round's traffic
-timeout -k 10 300 python3 bench.py --precision "$PREC" --steps $STEPS > "$OUT/bench.log" 2>&1 || exit $?
+ARGS="--config $CFG --precision $PREC --steps 1 --warmup 0 --cpu-seconds 0 --other-precision 0"
+SQ="SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CU_CYCLES SQ_INSTS_VALU_FMA_F32 GRBM_GUI_ACTIVE"
+pass() {   # name, counters, command...
+  local name=$1 ctr=$2; shift 2
+  timeout -s KILL 240 rocprofv3 --pmc $ctr -d "$OUT/$name" -o run --output-format csv -- "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" >> "$OUT/status.txt"
+  return $rc
+}
+pass pmc_fetch FETCH_SIZE python3 bench.py $ARGS || exit 1
+pass pmc_write WRITE_SIZE python3 bench.py $ARGS || exit 1
+pass pmc_sq "$SQ" python3 bench.py $ARGS || exit 1
+if [ -x tools/bin/ubench_valu ]; then pass ubench_sq "$SQ" ./tools/bin/ubench_valu || exit 1; fi
+python3 tools/pmc_round.py "$OUT" "$CFG:$PREC:1" > "$OUT/pmc_summary.txt" 2>&1 || exit 1
+timeout -k 10 300 python3 bench.py --config "$CFG" --precision "$PREC" --steps 10 --warmup 2 --pmc "$OUT/pmc.json" \
+    > "$OUT/bench.log" 2>&1 || exit 1
 grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- \
-    python3 bench.py --precision "$PREC" --steps $STEPS --cpu-seconds 0 > "$OUT/ktrace.log" 2>&1 || exit $?
+    python3 bench.py --config "$CFG" --precision "$PREC" --steps 10 --warmup 2 --cpu-seconds 0 --other-precision 0 \
+    --pmc "$OUT/pmc.json" > "$OUT/ktrace.log" 2>&1 || exit 1
+echo "profile_round done" >> "$OUT/status.txt"
