@@ -131,6 +131,8 @@ template <typename T> struct KParams {
     const float* rfsph;
     const float* ftop;
     const float* fsup;         // super boxes (4 clusters each), 4 per group
+    const float* fmeg;         // mega boxes (4 supers each), 4 per group; n_mg groups, 0: no mega level
+    uint32_t n_mg;
     const uint32_t* ridx;
     uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
@@ -393,7 +395,7 @@ __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_
     if (valid && (root < best_t || (root == best_t && (int)i > best))) { best_t = root; best = (int)i; }   // ties: later wins (:141)
 }
 
-template <typename T, bool root2, bool SCALAR = false, bool CAMT = false>
+template <typename T, bool root2, bool SCALAR = false, bool CAMT = false, bool MEGA = false>
 __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, const V3<T>& d, T& t_out) {
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254 (loop-invariant)
@@ -687,46 +689,68 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         }
         // Three levels: super boxes (4 clusters each, 4 per group) per chunk of 32 supers, then the
         // passing supers' cluster boxes (one group each), then the passing clusters' sphere groups.
+        // Scenes with more than 32 supers (config E: 157) test mega boxes (4 supers each) first, per
+        // chunk of 32, and only the passing megas' super groups.
         cptr<float> ft = (cptr<float>)__builtin_assume_aligned(qa.ftop, 32);
         cptr<float> fs = (cptr<float>)__builtin_assume_aligned(qa.fsup, 32);
         const uint32_t nsg = (ntop + 3u) / 4u;   // super groups (ntop supers, one per cluster top group)
-        for (uint32_t t0 = 0; t0 < nsg; t0 += 8u) {
-            uint32_t smask = 0;
-            n_box += min(8u, nsg - t0);
-            box_loop(fs + kBoxFloats * t0, min(8u, nsg - t0), [&](const BoxGroup& cur, uint32_t t) {
-                KSTAT(5);
-                smask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
-            });
-            while (smask != 0u) {
-                const uint32_t sup = 4u * t0 + (uint32_t)__builtin_ctz(smask);
-                smask &= smask - 1u;
-                // padding supers past the last one are empty boxes; a degenerate lane (all box times
-                // NaN) passes them, and they have no cluster boxes behind them
-                if (sup >= ntop) break;
-                KSTAT(5);
-                ++n_box;
-                uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
-                while (mask != 0u) {
-                    const uint32_t g0 = nxg + 4u * (4u * sup + (uint32_t)__builtin_ctz(mask));
-                    mask &= mask - 1u;
-                    KSTAT(4);
-                    n_filt += 4u;
-                    sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
-                        uint32_t s0, s1;
-                        // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
-                        // rejects them as well (the filter passes every sphere the reference can hit).
-                        if (__ballot(is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) != 0ull) {
-                            // only the sphere pairs some lane passes (one compare each, taken groups only)
-                            uint32_t pairs = 3u;
+        // the clusters of one passing super: its group of 4 cluster boxes, then their sphere groups
+        auto walk_super = [&](uint32_t sup) {
+            KSTAT(5);
+            ++n_box;
+            uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
+            while (mask != 0u) {
+                const uint32_t g0 = nxg + 4u * (4u * sup + (uint32_t)__builtin_ctz(mask));
+                mask &= mask - 1u;
+                KSTAT(4);
+                n_filt += 4u;
+                sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
+                    uint32_t s0, s1;
+                    // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
+                    // rejects them as well (the filter passes every sphere the reference can hit).
+                    if (__ballot(is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) != 0ull) {
+                        // only the sphere pairs some lane passes (one compare each, taken groups only)
+                        uint32_t pairs = 3u;
 #ifndef RT_EXP_PAIRS_F64
-                            if constexpr (sizeof(T) == 4)
+                        if constexpr (sizeof(T) == 4)
 #endif
-                                pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
-                                        (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
-                            n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
-                            exact4(g0 + g, pairs);
-                        }
-                    });
+                            pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
+                                    (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
+                        n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
+                        exact4(g0 + g, pairs);
+                    }
+                });
+            }
+        };
+        // The top level is the super boxes, or (MEGA: scenes with more than 8 super groups, config E)
+        // the mega boxes; chunks of 8 top groups (32 boxes) give a 32-bit wave mask of the passing
+        // top boxes.  A mega box nd covers super group nd.
+        cptr<float> fu = MEGA ? (cptr<float>)__builtin_assume_aligned(qa.fmeg, 32) : fs;
+        const uint32_t ntg = MEGA ? qa.n_mg : nsg, ntn = MEGA ? nsg : ntop;   // top groups, top boxes
+        for (uint32_t t0 = 0; t0 < ntg; t0 += 8u) {
+            uint32_t tmask = 0;
+            n_box += min(8u, ntg - t0);
+            box_loop(fu + kBoxFloats * t0, min(8u, ntg - t0), [&](const BoxGroup& cur, uint32_t t) {
+                KSTAT(5);
+                tmask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
+            });
+            while (tmask != 0u) {
+                const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);
+                tmask &= tmask - 1u;
+                // padding boxes past the last one are empty; a degenerate lane (all box times NaN)
+                // passes them, and nothing lies behind them
+                if (nd >= ntn) break;
+                if constexpr (MEGA) {
+                    ++n_box;
+                    uint32_t smask = box_mask(load_box(fs, nd), B0, B1, B2, B3, B4);
+                    while (smask != 0u) {
+                        const uint32_t sup = 4u * nd + (uint32_t)__builtin_ctz(smask);
+                        smask &= smask - 1u;
+                        if (sup >= ntop) break;
+                        walk_super(sup);
+                    }
+                } else {
+                    walk_super(nd);
                 }
             }
         }
@@ -1500,7 +1524,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
 // pop them as rays whose bounce-0 scatter is pending.  Every ray still meets every sphere.
 constexpr uint32_t kQCap = 128;   // camera-batch queue entries per wave (a batch adds at most 64)
 
-template <typename T, int W, bool ROOT2, int MODE = kModeV2, bool CAMQ = false>
+template <typename T, int W, bool ROOT2, int MODE = kModeV2, bool CAMQ = false, bool MEGA = false>
 __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     constexpr bool SC = MODE == kModeScalar;
     constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? kQCap : 1;
@@ -1792,11 +1816,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             V3<T> o2 = o;
             asm volatile("" : "+v"(o2.x));
             T t2;
-            const int h2 = nearest_hit<T, ROOT2, SC>(p, o2, d, t2);
+            const int h2 = nearest_hit<T, ROOT2, SC, false, MEGA>(p, o2, d, t2);
             asm volatile("" ::"v"(h2), "v"(t2));
         }
 #endif
-        if (act) hit_i = nearest_hit<T, ROOT2, SC>(p, o, d, hit_t);
+        if (act) hit_i = nearest_hit<T, ROOT2, SC, false, MEGA>(p, o, d, hit_t);
         const unsigned long long bact = __ballot(act);
         if (lane == 0 && bact) { wcount[wave][0] += (uint32_t)__popcll(bact); wcount[wave][1] += 64u; }
         // ---- terminations: record e (and the colour of a sky hit) ----
@@ -1858,6 +1882,8 @@ struct rt_context {
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
     void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
+    void* meg64 = nullptr; void* meg32 = nullptr;   // mega boxes (4 supers each; big scenes only)
+    uint32_t n_mg = 0;
     uint32_t* ridx = nullptr;
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
     void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
@@ -1951,6 +1977,9 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
     (void)hipFree(c->sup64); (void)hipFree(c->sup32);
     c->sup64 = c->sup32 = nullptr;
+    (void)hipFree(c->meg64); (void)hipFree(c->meg32);
+    c->meg64 = c->meg32 = nullptr;
+    c->n_mg = 0;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
     c->clus64 = c->clus32 = c->cullc64 = c->cullc32 = nullptr;
     c->n_cslots = c->n_clp = 0;
@@ -2160,7 +2189,7 @@ static SweepLayout build_layout(const rt_scene* s) {
 template <typename T>
 static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec, const SweepLayout& L,
                        std::vector<T>& rgrp, std::vector<float>& rfgrp, std::vector<float>& top, float& cmax,
-                       float& r2max, std::vector<float>& sup) {
+                       float& r2max, std::vector<float>& sup, std::vector<float>& meg) {
     auto up32 = [](double v) -> float {
         float f = (float)v;
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
@@ -2217,38 +2246,45 @@ static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec
         for (int f = 0; f < 6; ++f) top[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
     }
     // Super boxes: the union of the 4 cluster boxes of each top group, same rounding; 4 per group,
-    // padded with empty boxes plus one empty group (prefetch target).
-    const size_t nsup = nc / 4, nsg = (nsup + 3) / 4;
-    sup.assign((size_t)kBoxFloats * (nsg + 1), 0.0f);
-    for (size_t k = 0; k < 4 * (nsg + 1); ++k) {
-        float b[6] = {0.0f, 0.0f, 0.0f, -INFINITY, -INFINITY, -INFINITY};
-        if (k < nsup) {
-            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-            bool inf = false, any = false;
-            for (size_t j = 0; j < 4; ++j) {
-                const float* t = &top[kBoxFloats * k + 12 * (j / 2) + (j % 2)];
-                if (!(t[6] > -INFINITY)) continue;   // empty cluster
-                any = true;
-                for (int a = 0; a < 3; ++a) {
-                    if (!(t[6 + 2 * a] < INFINITY)) inf = true;
-                    lo[a] = std::min(lo[a], (double)t[2 * a] - (double)t[6 + 2 * a]);
-                    hi[a] = std::max(hi[a], (double)t[2 * a] + (double)t[6 + 2 * a]);
+    // padded with empty boxes plus one empty group (prefetch target).  Mega boxes likewise over the
+    // 4 supers of each super group, when there are more than 8 super groups (one sweep chunk).
+    auto unite = [&](const std::vector<float>& lower, size_t nup, std::vector<float>& upper) {
+        const size_t ng = (nup + 3) / 4;
+        upper.assign((size_t)kBoxFloats * (ng + 1), 0.0f);
+        for (size_t k = 0; k < 4 * (ng + 1); ++k) {
+            float b[6] = {0.0f, 0.0f, 0.0f, -INFINITY, -INFINITY, -INFINITY};
+            if (k < nup) {
+                double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                bool inf = false, any = false;
+                for (size_t j = 0; j < 4; ++j) {
+                    const float* t = &lower[kBoxFloats * k + 12 * (j / 2) + (j % 2)];
+                    if (!(t[6] > -INFINITY)) continue;   // empty box
+                    any = true;
+                    for (int a = 0; a < 3; ++a) {
+                        if (!(t[6 + 2 * a] < INFINITY)) inf = true;
+                        lo[a] = std::min(lo[a], (double)t[2 * a] - (double)t[6 + 2 * a]);
+                        hi[a] = std::max(hi[a], (double)t[2 * a] + (double)t[6 + 2 * a]);
+                    }
+                }
+                if (any) {
+                    double c1 = 0.0;
+                    for (int a = 0; a < 3; ++a) {
+                        b[a] = inf ? 0.0f : (float)(0.5 * (lo[a] + hi[a]));
+                        const double h = std::max(hi[a] - (double)b[a], (double)b[a] - lo[a]);
+                        b[3 + a] = inf ? INFINITY : up32(h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a]));
+                        c1 += std::fabs((double)b[a]) + (double)b[3 + a];
+                    }
+                    if (!inf) cm = std::max(cm, c1);
                 }
             }
-            if (any) {
-                double c1 = 0.0;
-                for (int a = 0; a < 3; ++a) {
-                    b[a] = inf ? 0.0f : (float)(0.5 * (lo[a] + hi[a]));
-                    const double h = std::max(hi[a] - (double)b[a], (double)b[a] - lo[a]);
-                    b[3 + a] = inf ? INFINITY : up32(h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a]));
-                    c1 += std::fabs((double)b[a]) + (double)b[3 + a];
-                }
-                if (!inf) cm = std::max(cm, c1);
-            }
+            const size_t tg = k / 4, j = k % 4;
+            for (int f = 0; f < 6; ++f) upper[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
         }
-        const size_t tg = k / 4, j = k % 4;
-        for (int f = 0; f < 6; ++f) sup[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
-    }
+    };
+    const size_t nsup = nc / 4, nsg = (nsup + 3) / 4;
+    unite(top, nsup, sup);
+    if (nsg > 8) unite(sup, nsg, meg);
+    else meg.clear();
     cmax = up32(cm);
     (void)r2max;
 }
@@ -2288,11 +2324,16 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->fsph64, f64g.data(), f64g.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
         const SweepLayout L = build_layout(s);
-        std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32, s64, s32;
-        pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64, s64);
-        pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32, s32);
+        std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32, s64, s32, m64, m32;
+        pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64, s64, m64);
+        pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32, s32, m32);
         if ((rc = up(&c->sup64, s64.data(), s64.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->sup32, s32.data(), s32.size() * sizeof(float))) != RT_OK) return rc;
+        c->n_mg = m32.empty() ? 0u : (uint32_t)(m32.size() / kBoxFloats - 1);   // groups, without the empty one
+        if (c->n_mg) {
+            if ((rc = up(&c->meg64, m64.data(), m64.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->meg32, m32.data(), m32.size() * sizeof(float))) != RT_OK) return rc;
+        }
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
         c->n_xs = L.n_xs;
@@ -2372,20 +2413,20 @@ static bool check_range(const rt_camera* cam, const rt_tile_range* r) {
 
 static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
 
-// The kernel instantiation for (flags, waves-per-SIMD target, camera batches).
+// The kernel instantiation for (flags, waves-per-SIMD target, camera batches, mega level).  The mega
+// level (scenes with more than 8 super groups) has its own live-path kernels at the default W; other
+// kernels sweep such scenes from the super boxes (the same result, more box tests).
 template <typename T, bool CAMQ>
-static void (*pick_kernel(uint32_t flags, int W))(KParams<T>) {
+static void (*pick_kernel(uint32_t flags, int W, bool mega))(KParams<T>) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
-    constexpr int WM = kWavesModes<T>;
+    constexpr int WM = kWavesModes<T>, WD = sizeof(T) == 4 ? kWavesF32 : kWavesF64;
     if (flags & RT_FLAG_MODE_SCALAR) return trace_paths<T, WM, false, kModeScalar, CAMQ>;
     if (flags & RT_FLAG_MODE_VECTORIZED)
         return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
     if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
-    if (!CAMQ)
-        return W >= 6 ? trace_paths<T, 6, false, kModeV2, false> : W >= 5 ? trace_paths<T, 5, false, kModeV2, false>
-                                                                  : trace_paths<T, 4, false, kModeV2, false>;
-    return W >= 8 ? trace_paths<T, 8, false, kModeV2, true> : W >= 6 ? trace_paths<T, 6, false, kModeV2, true>
-         : W >= 5 ? trace_paths<T, 5, false, kModeV2, true> : trace_paths<T, 4, false, kModeV2, true>;
+    if (mega && W == WD) return trace_paths<T, WD, false, kModeV2, CAMQ, true>;
+    return W >= 6 ? trace_paths<T, 6, false, kModeV2, CAMQ> : W >= 5 ? trace_paths<T, 5, false, kModeV2, CAMQ>
+                                                           : trace_paths<T, 4, false, kModeV2, CAMQ>;
 }
 
 template <typename T>
@@ -2403,6 +2444,8 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
     p.ftop = (const float*)(f64 ? c->top64 : c->top32);
     p.fsup = (const float*)(f64 ? c->sup64 : c->sup32);
+    p.fmeg = (const float*)(f64 ? c->meg64 : c->meg32);
+    p.n_mg = c->n_mg;
     p.ridx = c->ridx;
     p.n_top = c->n_top;
     p.n_xg = c->n_xg;
@@ -2468,7 +2511,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : sizeof(T) == 8 ? kWavesF64 : kWavesF32;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
-    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W) : pick_kernel<T, false>(flags, W);
+    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0) : pick_kernel<T, false>(flags, W, p.n_mg > 0);
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
         p.camf = (const float*)(f64 ? c->camf64 : c->camf32);

@@ -169,3 +169,21 @@ def test_work_counters(renderer):
     _, _, d64 = render(renderer, flat, cam, 50, 64, 0)
     g32, g64 = abi.executed_flop(d64, "f64")
     assert g64 > 0 and g32 > 0
+
+
+# ---------------------------------------------------------------- big scenes: the mega-box level
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_config_e_filter_off_same_image(renderer, monkeypatch, flags):
+    """Config E's 10 000 spheres take the four-level general sweep (mega boxes over 4 supers each):
+    every box level on and off (RT_FILTER_OFF: every lane degenerate, every box passes) must give the
+    oracle's image, pixel for pixel."""
+    flat = rt.scenes.config_scene("E").flatten()
+    cam = cam_for(24, 14)
+    _, lin_on, st_on = render(renderer, flat, cam, 50, 32, flags)
+    _, lin_o, segs_o, _ = oracle_render(flat, cam, 50, 32, SEED, 0, precision="f32" if flags else "f64")
+    np.testing.assert_array_equal(lin_on, lin_o)
+    assert st_on.ray_segments == segs_o
+    monkeypatch.setenv("RT_FILTER_OFF", "1")
+    _, lin_off, st_off = render(renderer, flat, cam, 50, 32, flags)
+    np.testing.assert_array_equal(lin_off, lin_o)
+    assert st_off.box_groups > st_on.box_groups and st_off.filter_groups > st_on.filter_groups
