@@ -122,7 +122,8 @@ template <typename T> struct KParams {
     float f_r2min;             // min r2f over non-exact spheres (after the host's floor)
     float f_ir2, f_hir2, f_isr; // 1/r2min, 0.5/r2min and 8 u/sqrt(r2min), rounded up (launch_t)
     const float* cull;         // camera cone-cull records {wx, wy, wz, rp} per slot of the sweep layout
-    const float* cullc;        // ... and per cluster (build_cam_table)
+    const float* cullc;        // ... and per cluster, then per super (build_cam_table)
+    uint32_t n_clp, n_supc;    // cluster records (x64), super records after them (x64; 0: none)
     const T* camx;             // camera-origin table per sphere {ocx, ocy, ocz, c} (AoS; build_cam_table)
     // general sweep, two-level (build_layout / pack_sweep): slot-order exact and filter streams,
     // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), slot -> scene index; n_top top groups,
@@ -796,7 +797,7 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
-template <typename T, bool root2, bool SCALAR>
+template <typename T, bool root2, bool SCALAR, bool MEGA = false>
 __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const uint32_t lane = threadIdx.x & 63u;
     const unsigned long long vm = __ballot(v);
@@ -880,16 +881,15 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
         }
     }
     // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
-    // to 4 passing clusters per pass, 16 lanes each
-    for (uint32_t cb = 0; cb < ncl; cb += 64u) {
-        ++n_cone;
-        unsigned long long M = __ballot(cone(cb == 0 ? kw0 : cc[cb + lane]));   // padded to whole 64s
+    // to 4 passing clusters per pass, 16 lanes each.  M: ballot of a cluster test in which lane L
+    // tested cluster klane(L).
+    auto members = [&](unsigned long long M, uint32_t klane) {
         while (M != 0ull) {
             ++n_cone;
             uint32_t k[4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {   // empty quarters take the padding cluster ncl (all dummies)
-                k[j] = M != 0ull ? cb + (uint32_t)__builtin_ctzll(M) : ncl;
+                k[j] = M != 0ull ? (uint32_t)__builtin_amdgcn_readlane(klane, (int)__builtin_ctzll(M)) : ncl;
                 M &= M - 1ull;
             }
             const uint32_t qd = lane >> 4;
@@ -901,6 +901,33 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
                 m &= m - 1ull;
                 const uint32_t kb = (b >> 4) == 0 ? k[0] : (b >> 4) == 1 ? k[1] : (b >> 4) == 2 ? k[2] : k[3];
                 exact(nx + 16u * kb + (b & 15u));
+            }
+        }
+    };
+    const uint32_t nsu = MEGA ? q.n_supc : 0u;   // the super level exists only in the MEGA kernels
+    if (nsu == 0u) {
+        for (uint32_t cb = 0; cb < ncl; cb += 64u) {
+            ++n_cone;
+            members(__ballot(cone(cb == 0 ? kw0 : cc[cb + lane])), cb + lane);   // padded to whole 64s
+        }
+    } else {
+        // big scenes: lanes as supers first (their records, after the clusters', bound every member
+        // sphere's record the same way), then the 4 clusters of up to 16 passing supers per pass
+        const float4* csu = cc + q.n_clp;
+        for (uint32_t sb = 0; sb < nsu; sb += 64u) {
+            ++n_cone;
+            unsigned long long S = __ballot(cone(csu[sb + lane]));   // padded to whole 64s (rp = -inf)
+            while (S != 0ull) {
+                uint32_t mys = 0xFFFFFFFFu;
+                for (uint32_t j = 0; j < 16u && S != 0ull; ++j) {
+                    const uint32_t sj = sb + (uint32_t)__builtin_ctzll(S);
+                    S &= S - 1ull;
+                    if ((lane >> 2) == j) mys = sj;
+                }
+                const bool have = mys != 0xFFFFFFFFu;
+                const uint32_t kl = have ? 4u * mys + (lane & 3u) : ncl;
+                ++n_cone;
+                members(__ballot(have && cone(cc[kl])), kl);
             }
         }
     }
@@ -1721,11 +1748,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             V3<T> bd2 = bd;
             asm volatile("" : "+v"(bd2.x));
             T bt2;
-            const int bi2 = camera_sweep<T, ROOT2, SC>(v, bd2, bt2);
+            const int bi2 = camera_sweep<T, ROOT2, SC, MEGA>(v, bd2, bt2);
             asm volatile("" ::"v"(bi2), "v"(bt2));
         }
 #endif
-        bi = camera_sweep<T, ROOT2, SC>(v, bd, bt);   // whole wave: lanes are spheres in the cull
+        bi = camera_sweep<T, ROOT2, SC, MEGA>(v, bd, bt);   // whole wave: lanes are spheres in the cull
 #else
         if (v) bi = nearest_hit<T, ROOT2, SC, true>(p, bd, bd, bt);
 #endif
@@ -1888,6 +1915,7 @@ struct rt_context {
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
     void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
     uint32_t n_cslots = 0, n_clp = 0;                 // slot-order cull records; cluster records (x64)
+    uint32_t n_supc = 0;                              // super records after them (x64; 0: none)
     uint32_t n_top = 0, n_xg = 0, n_xs = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
@@ -1982,7 +2010,7 @@ static void free_scene(rt_context* c) {
     c->n_mg = 0;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
     c->clus64 = c->clus32 = c->cullc64 = c->cullc32 = nullptr;
-    c->n_cslots = c->n_clp = 0;
+    c->n_cslots = c->n_clp = c->n_supc = 0;
     c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
     c->ridx = nullptr;
     c->n_top = c->n_xg = c->n_xs = 0;
@@ -2345,30 +2373,41 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         std::vector<uint32_t> ridx(c->n_cslots, 0xFFFFFFFFu);
         for (size_t i = 0; i < L.slot.size(); ++i) if (L.slot[i] >= 0) ridx[i] = (uint32_t)L.slot[i];
         // cluster bounding spheres for the camera cull, per precision: centre = the members' AABB
-        // centre, R >= max |c_i - C| + |r_i| over the members' T-precision centres and radii
+        // centre, R >= max |c_i - C| + |r_i| over the members' T-precision centres and radii.  Scenes
+        // with more than 128 clusters (config E) also get super records, the bounding spheres of the
+        // 4 clusters of each super (camera_sweep tests them first), stored after the cluster records.
+        const uint32_t nsup = ncl / 4u;
+        c->n_supc = ncl > 128u ? (nsup + 63u) / 64u * 64u : 0u;
         auto bounds = [&](auto const& cen, std::vector<double>& out) {
-            out.assign((size_t)4 * (c->n_clp ? c->n_clp : 1), 0.0);
+            out.assign((size_t)4 * ((c->n_clp + c->n_supc) ? c->n_clp + c->n_supc : 1), 0.0);
             for (size_t k = 0; k < out.size() / 4; ++k) out[4 * k + 3] = -INFINITY;
-            for (uint32_t k = 0; k < ncl; ++k) {
-                const auto& m = L.members[k];
-                if (m.empty()) continue;
+            auto sphere = [&](size_t at, uint32_t k0, uint32_t nk) {   // the members of clusters k0 .. k0+nk-1
                 double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                for (uint32_t i : m)
-                    for (int a = 0; a < 3; ++a) {
-                        const double r = std::fabs((double)cen[4 * i + 3]);
-                        lo[a] = std::min(lo[a], (double)cen[4 * i + a] - r);
-                        hi[a] = std::max(hi[a], (double)cen[4 * i + a] + r);
+                bool any = false;
+                for (uint32_t k = k0; k < k0 + nk; ++k)
+                    for (uint32_t i : L.members[k]) {
+                        any = true;
+                        for (int a = 0; a < 3; ++a) {
+                            const double r = std::fabs((double)cen[4 * i + 3]);
+                            lo[a] = std::min(lo[a], (double)cen[4 * i + a] - r);
+                            hi[a] = std::max(hi[a], (double)cen[4 * i + a] + r);
+                        }
                     }
+                if (!any) return;
                 double C[3], R = 0.0;
                 for (int a = 0; a < 3; ++a) C[a] = 0.5 * (lo[a] + hi[a]);
-                for (uint32_t i : m) {
-                    const double dx = (double)cen[4 * i] - C[0], dy = (double)cen[4 * i + 1] - C[1],
-                                 dz = (double)cen[4 * i + 2] - C[2];
-                    R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs((double)cen[4 * i + 3]));
-                }
-                out[4 * k] = C[0]; out[4 * k + 1] = C[1]; out[4 * k + 2] = C[2];
-                out[4 * k + 3] = std::isfinite(R) ? R * (1.0 + 0x1.0p-40) : INFINITY;
-            }
+                for (uint32_t k = k0; k < k0 + nk; ++k)
+                    for (uint32_t i : L.members[k]) {
+                        const double dx = (double)cen[4 * i] - C[0], dy = (double)cen[4 * i + 1] - C[1],
+                                     dz = (double)cen[4 * i + 2] - C[2];
+                        R = std::max(R, std::sqrt(dx * dx + dy * dy + dz * dz) + std::fabs((double)cen[4 * i + 3]));
+                    }
+                out[4 * at] = C[0]; out[4 * at + 1] = C[1]; out[4 * at + 2] = C[2];
+                out[4 * at + 3] = std::isfinite(R) ? R * (1.0 + 0x1.0p-40) : INFINITY;
+            };
+            for (uint32_t k = 0; k < ncl; ++k) sphere(k, k, 1);
+            if (c->n_supc)
+                for (uint32_t k = 0; k < nsup; ++k) sphere(c->n_clp + k, 4 * k, 4);
         };
         std::vector<double> cl64, cl32;
         bounds(c64, cl64);
@@ -2519,12 +2558,15 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         p.cull = (const float*)(f64 ? c->cull64 : c->cull32);
         const uint32_t n_slots = (p.n_groups + 1) * kGroup<T>, n_fslots = (p.n_fgroups + 1) * 4;
         p.cullc = (const float*)(f64 ? c->cullc64 : c->cullc32);
-        const uint32_t n_thr = std::max(std::max(std::max(n_slots, n_fslots), c->n_cull), std::max(c->n_cslots, c->n_clp));
+        p.n_clp = c->n_clp;
+        p.n_supc = c->n_supc;
+        const uint32_t n_thr = std::max(std::max(std::max(n_slots, n_fslots), c->n_cull),
+                                        std::max(c->n_cslots, c->n_clp + c->n_supc));
         auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
         hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
                            (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off,
                            (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres, c->ridx, c->n_cslots,
-                           (const double*)(f64 ? c->clus64 : c->clus32), (float*)p.cullc, c->n_clp);
+                           (const double*)(f64 ? c->clus64 : c->clus32), (float*)p.cullc, c->n_clp + c->n_supc);
         HIPCHK(hipGetLastError());
     }
     int per_cu = 0;
