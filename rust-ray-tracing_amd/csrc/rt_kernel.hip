@@ -38,6 +38,7 @@
 #include <limits>
 #include <mutex>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/rt_mi355x.h"
@@ -349,13 +350,31 @@ __device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2
         : [ux] "=&v"(ux), [uy] "=&v"(uy), [uz] "=&v"(uz), [nx] "=&v"(nx), [ny] "=&v"(ny), [nz] "=&v"(nz)
         : [cx] "s"(cx), [cy] "s"(cy), [cz] "s"(cz), [hx] "s"(hx), [hy] "s"(hy), [hz] "s"(hz), [B0] "v"(B0),
           [B1] "v"(B1), [B2] "v"(B2), [B3] "v"(B3), [B4] "v"(B4));
-    auto pass = [](float nx, float ny, float nz, float fx, float fy, float fz) -> bool {
-        const float tn = fmaxf(fmaxf(nx, ny), nz), tf = fminf(fminf(fx, fy), fz);
-        return !(tf - tn < 0.0f) && !(tf < 0.0f);
+    // Culled iff tf < tn or tf < 0, i.e. iff tf < max(tn, 0) (NaN: kept).  Inline asm down to the
+    // wave mask: fmaxf / fminf on the asm's outputs made the compiler canonicalise each input first
+    // (two v_max_f32 x, x per box; these values come from FMAs, never signalling NaNs), and the
+    // ballot's bool took a round trip through a VGPR.  v_cmp_e64 writes 0 for inactive lanes, as a
+    // ballot does.
+    auto pass = [](float nx, float ny, float nz, float fx, float fy, float fz, auto bitc) -> uint32_t {
+        constexpr uint32_t bit = decltype(bitc)::value;
+        float tn, tf;
+        unsigned long long m;
+        uint32_t r;
+        asm volatile(
+            "v_max3_f32 %[tn], %[nx], %[ny], %[nz]\n\t"
+            "v_min3_f32 %[tf], %[fx], %[fy], %[fz]\n\t"
+            "v_max_f32 %[tn], 0, %[tn]\n\t"
+            "v_cmp_nlt_f32_e64 %[m], %[tf], %[tn]\n\t"
+            "s_cmp_lg_u64 %[m], 0\n\t"
+            "s_cselect_b32 %[r], %[bit], 0"
+            : [tn] "=&v"(tn), [tf] "=&v"(tf), [m] "=&s"(m), [r] "=s"(r)
+            : [nx] "v"(nx), [ny] "v"(ny), [nz] "v"(nz), [fx] "v"(fx), [fy] "v"(fy), [fz] "v"(fz), [bit] "n"(bit)
+            : "scc");
+        return r;
     };
-    const uint32_t m0 = __ballot(pass(nx.x, ny.x, nz.x, ux.x, uy.x, uz.x)) != 0ull ? 1u : 0u;
-    const uint32_t m1 = __ballot(pass(nx.y, ny.y, nz.y, ux.y, uy.y, uz.y)) != 0ull ? 2u : 0u;
-    return m0 | m1;
+    // readfirstlane: the mask is wave-uniform (the compiler cannot see that through the asm)
+    return __builtin_amdgcn_readfirstlane(pass(nx.x, ny.x, nz.x, ux.x, uy.x, uz.x, std::integral_constant<uint32_t, 1>{}) |
+                                          pass(nx.y, ny.y, nz.y, ux.y, uy.y, uz.y, std::integral_constant<uint32_t, 2>{}));
 }
 __device__ __forceinline__ uint32_t box_mask(const BoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
     return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
