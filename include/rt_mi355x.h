@@ -108,12 +108,17 @@ typedef struct rt_stats {
  *   RT_FLAG_MODE_VECTORIZED: render_vectorized -> Scene::trace_vectorized (renderer.rs:102-139,
  *     ray_tracing.rs:312-373): each sample keeps its own value and the sky uses its own final
  *     direction (Q2, Q3 off); hit_packed is shared, so Q1 still applies unless RT_FLAG_ROOT2.
+ *   RT_FLAG_MODE_VECTORIZED3: render_vectorized3 -> Scene::trace_vectorized3 (renderer.rs:178-213,
+ *     ray_tracing.rs:508-628): each sample's own value as in _VECTORIZED, summed in the order an
+ *     in-place swap partition (CombinedIndex, :113-214, :561-607) leaves the slots in; the missing
+ *     lanes of a partial chunk add sky(0) (white at depth 0).
  *   RT_FLAG_MODE_SCALAR: TileRenderTask::render -> Scene::trace_rays (renderer.rs:68-100,
  *     ray_tracing.rs:264-306): scalar Sphere::hit (objects.rs:216-247; no FMA, both roots, normal
  *     divided by the signed radius), the first of equal hits wins (min_by_key), Color::average. */
 #define RT_FLAG_MODE_VECTORIZED 0x4u
 #define RT_FLAG_MODE_SCALAR 0x8u
-#define RT_FLAG_ALL 0xFu      /* any other bit is RT_ERR_INVALID */
+#define RT_FLAG_MODE_VECTORIZED3 0x10u
+#define RT_FLAG_ALL 0x1Fu     /* any other bit, or two mode bits, is RT_ERR_INVALID */
 
 /* Camera::new (ray_tracing.rs:27-62).  view_angle and defocus_angle in degrees. */
 int rt_camera_new(rt_camera* out, uint32_t image_width, uint32_t image_height, double focal_length,

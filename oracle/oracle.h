@@ -63,6 +63,10 @@ typedef struct or_camera {
  *               first minimum wins ties, Color::average in sample order. */
 #define OR_FLAG_MODE_VECTORIZED 0x4u
 #define OR_FLAG_MODE_SCALAR 0x8u
+/* OR_FLAG_MODE_VECTORIZED3: TileRenderTask::render_vectorized3 -> Scene::trace_vectorized3
+ *               (renderer.rs:178-213, ray_tracing.rs:508-628): in-place swap partition, own-direction
+ *               sky, colours white for every lane (missing lanes of a partial chunk add sky(0)). */
+#define OR_FLAG_MODE_VECTORIZED3 0x10u
 
 /* Render the listed pixels (global index row*W+col; NULL = all W*H in order).
  * rgb_out: n*3 bytes, lin_out: n*3 doubles (pixel colour after /spp, before

@@ -415,6 +415,111 @@ static void SFX(trace_pixel)(const SFX(scene_r)* S, SFX(ws)* w, uint32_t depth, 
     *segs += nseg;
 }
 
+/* ---- "vectorized3" mode: Scene::trace_vectorized3, ray_tracing.rs:508-628 (N = 4), as called by
+ * render_vectorized3 (renderer.rs:178-213).  Literal: one buffer, colours start white for every lane
+ * (:515), the chunks [0, num_active) are traced, then an in-place swap partition with CombinedIndex
+ * (:113-214, :561-607): the next disabled slot from the front (over ALL chunks) swaps with the previous
+ * enabled slot from the back (below num_active) while the front's chunk is below the back's; the final
+ * sky uses each slot's own (final) direction and the sum is per lane over chunks (:611-627). ---- */
+/* CombinedIndex::increment / decrement (:129-171); slot 4 = before_first (:121-123) */
+static inline int SFX(ci_inc)(uint32_t C, uint32_t* c, uint32_t* l) {
+    if (*l >= 4u) { if (C > 0) { *c = 0; *l = 0; return 1; } return 0; }
+    if (*l < 3u) { *l += 1; return 1; }
+    if (*c + 1 < C) { *c += 1; *l = 0; return 1; }
+    return 0;
+}
+static inline int SFX(ci_dec)(uint32_t* c, uint32_t* l) {
+    if (*l > 0) { *l -= 1; return 1; }
+    if (*c > 0) { *c -= 1; *l = 3; return 1; }
+    return 0;
+}
+static void SFX(trace_pixel_v3)(const SFX(scene_r)* S, SFX(ws)* w, uint32_t depth, uint32_t pix,
+                                uint32_t k0, uint32_t k1, uint32_t flags, REAL out[3], uint64_t* segs) {
+    const uint32_t C = w->C;
+    SFX(prays)* R = w->buf[0];
+    SFX(pcol)* col = w->col[0];
+    int* sky = w->sky[0];
+    for (uint32_t j = 0; j < C; ++j) {                                                /* :515-516 */
+        R[j] = w->rays0[j];
+        for (int l = 0; l < 4; ++l) { col[j].r[l] = 1; col[j].g[l] = 1; col[j].b[l] = 1; sky[j * 4 + l] = 0; }
+    }
+    uint32_t na = C;                                                                  /* :518 */
+    uint64_t nseg = 0;
+    for (uint32_t k = 0; k < depth; ++k) {                                            /* :520 */
+        if (na == 0) break;                                                           /* :521-524 */
+        for (uint32_t j = 0; j < na; ++j) {                                           /* :526-559 */
+            SFX(phit) H;
+            for (int l = 0; l < 4; ++l) {
+                H.t[l] = (REAL)INFINITY; H.hit[l] = 0; H.front[l] = 0; H.mat[l] = 0;
+                H.nx[l] = H.ny[l] = H.nz[l] = 0;
+                nseg += (uint64_t)R[j].en[l];
+            }
+            for (uint32_t i = 0; i < S->n; ++i)
+                SFX(hit_packed)(&R[j], S->cx[i], S->cy[i], S->cz[i], S->r[i], S->mat[i], &H, flags);
+            SFX(finalize)(&R[j], &H);
+            for (int l = 0; l < 4; ++l) {
+                if (H.hit[l]) {
+                    V3 d = SFX(mk)(R[j].dx[l], R[j].dy[l], R[j].dz[l]);
+                    V3 p = SFX(mk)(H.px[l], H.py[l], H.pz[l]);
+                    V3 n = SFX(mk)(H.nx[l], H.ny[l], H.nz[l]);
+                    V3 nd;
+                    REAL att[3];
+                    SFX(scatter)(&S->mats[H.mat[l]], d, p, n, H.front[l], pix, R[j].sid[l], k, k0, k1, &nd, att);
+                    col[j].r[l] = col[j].r[l] * att[0];                               /* :542-543 */
+                    col[j].g[l] = col[j].g[l] * att[1];
+                    col[j].b[l] = col[j].b[l] * att[2];
+                    R[j].ox[l] = p.x; R[j].oy[l] = p.y; R[j].oz[l] = p.z;             /* :546 update() */
+                    R[j].dx[l] = nd.x; R[j].dy[l] = nd.y; R[j].dz[l] = nd.z;
+                    R[j].en[l] = 1;
+                } else {                                                              /* :553-556 */
+                    R[j].en[l] = 0;
+                    sky[j * 4 + l] = 1;
+                }
+            }
+        }
+        /* :563-607 swap partition */
+        uint32_t fc = 0, fl = 4, bc = na, bl = 0;                                     /* before_first; (na, 0) */
+        for (;;) {
+            int found = 0;                                                            /* next_disabled */
+            while (SFX(ci_inc)(C, &fc, &fl)) if (!R[fc].en[fl]) { found = 1; break; }
+            if (!found) { na = C; break; }                                            /* :573 */
+            found = 0;                                                                /* previous_enabled */
+            while (SFX(ci_dec)(&bc, &bl)) if (R[bc].en[bl]) { found = 1; break; }
+            if (!found) { na = 0; break; }                                            /* :581 */
+            if (fc >= bc) { na = bc + 1; break; }                                     /* :586-589 */
+            /* :592-605: front takes back's ray (enabled), back takes front's (disabled); colours and
+             * hit_sky swap with them; the sample id travels with its ray (RNG key) */
+            SFX(prays) t = R[fc];
+            R[fc].ox[fl] = R[bc].ox[bl]; R[fc].oy[fl] = R[bc].oy[bl]; R[fc].oz[fl] = R[bc].oz[bl];
+            R[fc].dx[fl] = R[bc].dx[bl]; R[fc].dy[fl] = R[bc].dy[bl]; R[fc].dz[fl] = R[bc].dz[bl];
+            R[fc].sid[fl] = R[bc].sid[bl]; R[fc].en[fl] = 1;
+            R[bc].ox[bl] = t.ox[fl]; R[bc].oy[bl] = t.oy[fl]; R[bc].oz[bl] = t.oz[fl];
+            R[bc].dx[bl] = t.dx[fl]; R[bc].dy[bl] = t.dy[fl]; R[bc].dz[bl] = t.dz[fl];
+            R[bc].sid[bl] = t.sid[fl]; R[bc].en[bl] = 0;
+            REAL cr = col[fc].r[fl], cg = col[fc].g[fl], cb = col[fc].b[fl];
+            col[fc].r[fl] = col[bc].r[bl]; col[fc].g[fl] = col[bc].g[bl]; col[fc].b[fl] = col[bc].b[bl];
+            col[bc].r[bl] = cr; col[bc].g[bl] = cg; col[bc].b[bl] = cb;
+            int hs = sky[fc * 4 + fl];
+            sky[fc * 4 + fl] = sky[bc * 4 + bl];
+            sky[bc * 4 + bl] = hs;
+        }
+    }
+    REAL acc[3][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
+    for (uint32_t j = 0; j < C; ++j) {                                                /* :611-625 */
+        for (int l = 0; l < 4; ++l) {
+            REAL sk[3];
+            SFX(sky)(R[j].dy[l], sk);                                                 /* its own direction */
+            REAL cr = col[j].r[l], cg = col[j].g[l], cb = col[j].b[l];
+            if (sky[j * 4 + l]) { cr = cr * sk[0]; cg = cg * sk[1]; cb = cb * sk[2]; }
+            if (R[j].en[l]) { cr = 0; cg = 0; cb = 0; }
+            acc[0][l] = acc[0][l] + cr; acc[1][l] = acc[1][l] + cg; acc[2][l] = acc[2][l] + cb;
+        }
+    }
+    for (int ch = 0; ch < 3; ++ch)                                                    /* :627 PackedColor::sum */
+        out[ch] = (((REAL)0.0 + acc[ch][0]) + acc[ch][1] + acc[ch][2]) + acc[ch][3];
+    *segs += nseg;
+}
+
 /* ---- "vectorized" mode: Scene::trace_vectorized, ray_tracing.rs:312-373 (one PackedRays<4>
  * chunk, no shuffle), as called by render_vectorized (renderer.rs:102-139). ---- */
 static void SFX(trace_chunk_v1)(const SFX(scene_r)* S, SFX(prays) R, uint32_t depth, uint32_t pix,
@@ -597,6 +702,8 @@ static void* SFX(worker)(void* arg) {
                 }
                 for (int ch = 0; ch < 3; ++ch)
                     sum[ch] = (((REAL)0.0 + acc[ch][0]) + acc[ch][1] + acc[ch][2]) + acc[ch][3];
+            } else if (J->flags & OR_FLAG_MODE_VECTORIZED3) {
+                SFX(trace_pixel_v3)(J->S, &w, J->depth, pix, J->k0, J->k1, J->flags, sum, &segs);
             } else {
                 SFX(trace_pixel)(J->S, &w, J->depth, pix, J->k0, J->k1, J->flags, sum, &segs);
             }
@@ -621,7 +728,10 @@ int SFX(oracle_render)(const or_scene* sc, const or_camera* cam, uint32_t max_bo
                        const uint32_t* pixels, uint32_t n_pixels,
                        uint8_t* rgb_out, double* lin_out, uint64_t* segments, int n_threads) {
     if (!sc || !cam || spp == 0 || cam->image_width == 0 || cam->image_height == 0) return 1;
-    if ((flags & OR_FLAG_MODE_VECTORIZED) && (flags & OR_FLAG_MODE_SCALAR)) return 1;
+    {
+        const uint32_t modes = flags & (OR_FLAG_MODE_VECTORIZED | OR_FLAG_MODE_SCALAR | OR_FLAG_MODE_VECTORIZED3);
+        if (modes & (modes - 1u)) return 1;   /* at most one mode */
+    }
     if (sc->n_spheres && (!sc->center || !sc->radius || !sc->material || !sc->materials)) return 1;
     for (uint32_t i = 0; i < sc->n_spheres; ++i)
         if (sc->material[i] >= sc->n_materials) return 1;

@@ -848,9 +848,11 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     bool all = __ballot(v && !(dt > 0.5f)) != 0ull;   // some ray > 60 deg off the axis (or NaN)
     // non-negative floats (and NaN above +inf) order as integers
     const uint32_t sm = wave_max_dpp(__float_as_uint(s2));
-    const float S = ufl(__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f));
+    // v_sqrt_f32 (1 ulp) for the cone's sin, cos and each record's p: 2 u relative each, inside the
+    // 4 u inflation of sin and rp's 32 u |w| (tests/cone_cull_fuzz.c models them as +-1 ulp)
+    const float S = ufl(__builtin_fmaf(__builtin_amdgcn_sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f));
     if (!(S < 0.5f)) all = true;
-    const float Cc = ufl(sqrtf(__builtin_fmaf(-S, S, 1.0f)));
+    const float Cc = ufl(__builtin_amdgcn_sqrtf(__builtin_fmaf(-S, S, 1.0f)));
     cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
     cptr<uint32_t> ri = (cptr<uint32_t>)q.ridx;
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
@@ -864,7 +866,7 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
         const float t = __builtin_fmaf(wc.z, az, __builtin_fmaf(wc.y, ay, wc.x * ax));
         const float px = __builtin_fmaf(wc.y, az, -(wc.z * ay)), py = __builtin_fmaf(wc.z, ax, -(wc.x * az)),
                     pz = __builtin_fmaf(wc.x, ay, -(wc.y * ax));
-        const float pp = sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
+        const float pp = __builtin_amdgcn_sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
         const float f = __builtin_fmaf(pp, Cc, -(t * S));
         return wc.w > -INFINITY && (all || !(f > wc.w));   // NaN f passes
     };
@@ -1169,6 +1171,7 @@ enum Mode : int {
     kModeV2 = 0,       // render_vectorized2 -> trace_vectorized2 (the live path; quirks Q2, Q3)
     kModeV1 = 1,       // render_vectorized -> trace_vectorized (ray_tracing.rs:312-373): own value, final-ray sky
     kModeScalar = 2,   // render -> trace_rays (ray_tracing.rs:264-306) + Color::average
+    kModeV3 = 3,       // render_vectorized3 -> trace_vectorized3 (ray_tracing.rs:508-628): own value, swap order
 };
 
 // Per-wave scratch of trace_paths (HBM layout): the position map of the pixel being
@@ -1273,7 +1276,10 @@ __device__ __forceinline__ bool guided_block(uint32_t np, uint32_t T, uint32_t G
 
 // PScratch sizes: the map (u16, u32 past 65532 positions), the records (e u8, u32 when depth > 254).
 __host__ __device__ inline uint32_t paths_wide(uint32_t P, uint32_t depth) { return (depth > 254u ? 1u : 0u) | (P > 65532u ? 2u : 0u); }
-__host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t wide) { return (P * ((wide & 2u) ? 4u : 2u) + 255u) & ~255u; }
+__host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t wide, bool v3) {
+    return v3 ? (8u * P + 255u) & ~255u   // vectorized3: slot -> sample map + the swap tables (finish_pixel)
+              : (P * ((wide & 2u) ? 4u : 2u) + 255u) & ~255u;
+}
 __host__ __device__ inline uint32_t paths_sbytes(uint32_t P, uint32_t tsz, uint32_t wide) {
     return (P * (4u * tsz + ((wide & 1u) ? 4u : 1u)) + 255u) & ~255u;
 }
@@ -1415,6 +1421,69 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         }
     }
 #endif
+    // vectorized3 (ray_tracing.rs:508-628): replay the in-place swap partitions.  After bounce k the
+    // slots q < 4 L hold enabled rays iff their sample has e > k; with D the disabled slots ascending
+    // (all chunks, the front scan) and E the enabled slots descending (the back scan from L), the
+    // literal loop swaps D[j] with E[j] while chunk(D[j]) < chunk(E[j]) (monotone in j, since D rises
+    // and E falls), i.e. for j < J = max over chunk boundaries c of min(#D below c, #E at or above c),
+    // and stops with num_active = chunk(max(E[J], D[J-1])) + 1 (the previous enabled slot below the
+    // last swap; none disabled: all C chunks, :573; none enabled: 0, :581).  sig[q] = the sample at
+    // slot q (>= spp: a missing lane of a partial chunk); tabD[j], tabE[j]: the samples at D[j], E[j].
+    // tests/test_v3_partition.py checks this closed form against the literal loop.
+    if constexpr (MODE == kModeV3) {
+        uint32_t* sig = (uint32_t*)sc.base;
+        uint32_t* tabD = sig + P;
+        uint32_t* tabE = tabD + P / 2u;
+        for (uint32_t qi = lane; qi < P; qi += 64u) sig[qi] = qi;
+        wave_mem_sync();
+        uint32_t L = C;
+        for (uint32_t k = 0; k < K; ++k) {
+            auto enabled = [&](uint32_t qq, uint32_t smp) -> bool { return qq < 4u * L && smp < spp && sc.e(s, smp) > k; };
+            uint32_t nd = 0, ne = 0;
+            for (uint32_t qb = 0; qb < P; qb += 64u) {
+                const uint32_t qq = qb + lane;
+                const bool in = qq < P;
+                const bool en = in && enabled(qq, in ? sig[qq] : 0u);
+                nd += (uint32_t)__popcll(__ballot(in && !en));
+                ne += (uint32_t)__popcll(__ballot(en));
+            }
+            if (nd == 0u) { L = C; continue; }   // no disabled slot: next_disabled is None (:573)
+            if (ne == 0u) { L = 0; break; }      // no enabled slot: previous_enabled is None (:581)
+            uint32_t cd = 0, ce = 0, Jl = 0;
+            for (uint32_t qb = 0; qb < P; qb += 64u) {
+                const uint32_t qq = qb + lane;
+                const bool in = qq < P;
+                const uint32_t smp = in ? sig[qq] : 0u;
+                const bool en = in && enabled(qq, smp), dis = in && !en;
+                const unsigned long long bd = __ballot(dis), be = __ballot(en);
+                const uint32_t rd = cd + (uint32_t)__popcll(bd & lt_mask), rf = ce + (uint32_t)__popcll(be & lt_mask);
+                if (in && (qq & 3u) == 0u) Jl = max(Jl, min(rd, ne - rf));   // boundary c = qq / 4
+                if (dis && rd < P / 2u) tabD[rd] = smp;
+                if (en && ne - 1u - rf < P / 2u) tabE[ne - 1u - rf] = smp;
+                cd += (uint32_t)__popcll(bd);
+                ce += (uint32_t)__popcll(be);
+            }
+            const uint32_t J = __builtin_amdgcn_readfirstlane(wave_max(Jl));
+            wave_mem_sync();
+            cd = 0; ce = 0;
+            uint32_t back = 0;   // 1 + the slot the loop stops at from the back: E[J] or D[J-1]
+            for (uint32_t qb = 0; qb < P; qb += 64u) {
+                const uint32_t qq = qb + lane;
+                const bool in = qq < P;
+                const uint32_t smp = in ? sig[qq] : 0u;
+                const bool en = in && enabled(qq, smp), dis = in && !en;
+                const unsigned long long bd = __ballot(dis), be = __ballot(en);
+                const uint32_t rd = cd + (uint32_t)__popcll(bd & lt_mask), re = ne - 1u - (ce + (uint32_t)__popcll(be & lt_mask));
+                if (dis && rd < J) sig[qq] = tabE[rd];
+                if (en && re < J) sig[qq] = tabD[re];
+                if ((en && re == J) || (dis && rd + 1u == J)) back = max(back, qq + 1u);
+                cd += (uint32_t)__popcll(bd);
+                ce += (uint32_t)__popcll(be);
+            }
+            L = (__builtin_amdgcn_readfirstlane(wave_max(back)) - 1u) / 4u + 1u;
+            wave_mem_sync();
+        }
+    }
     uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
 #ifdef RT_EXP_SKIP_REPLAY
     for (uint32_t k = 0; k < 0u; ++k) {   // timing experiment only: results are wrong
@@ -1502,7 +1571,19 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         for (uint32_t qb = 0; qb < P; qb += 64u) {
             const uint32_t qq = qb + lane;
             T vr = T(0.0), vg = T(0.0), vb = T(0.0);
-            if (qq < P) {
+            if (qq < P && MODE == kModeV3) {
+                // the sample at slot qq: its own value; a missing lane (white, hit_sky at bounce 0
+                // with a zero direction) adds sky(0), or white when no bounce ran (:611-619)
+                const uint32_t m = ((const uint32_t*)sc.base)[qq];
+                if (m < spp) {
+                    const C3<T> cm = sc.c(s, m);
+                    vr = cm.x; vg = cm.y; vb = cm.z;
+                } else if (depth > 0u) {
+                    vr = s0.x; vg = s0.y; vb = s0.z;
+                } else {
+                    vr = T(1.0); vg = T(1.0); vb = T(1.0);
+                }
+            } else if (qq < P) {
                 if (qq >= spp) {
                     if (MODE == kModeV2) {
                         if (depth > 0u) { vr = s0.x; vg = s0.y; vb = s0.z; }
@@ -2479,6 +2560,8 @@ static void (*pick_kernel(uint32_t flags, int W, bool mega))(KParams<T>) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
     constexpr int WM = kWavesModes<T>, WD = sizeof(T) == 4 ? kWavesF32 : kWavesF64;
     if (flags & RT_FLAG_MODE_SCALAR) return trace_paths<T, WM, false, kModeScalar, CAMQ>;
+    if (flags & RT_FLAG_MODE_VECTORIZED3)
+        return r2 ? trace_paths<T, WM, true, kModeV3, CAMQ> : trace_paths<T, WM, false, kModeV3, CAMQ>;
     if (flags & RT_FLAG_MODE_VECTORIZED)
         return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
     if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
@@ -2603,7 +2686,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         p.blk_g = G;
     }
     p.swide = paths_wide(p.P, depth);
-    p.vbytes = paths_vbytes(p.P, p.swide);
+    p.vbytes = paths_vbytes(p.P, p.swide, (flags & RT_FLAG_MODE_VECTORIZED3) != 0u);
     p.sbytes = paths_sbytes(p.P, sizeof(T), p.swide);
     p.scratch_stride = (size_t)p.vbytes + (size_t)kSlots * p.sbytes;
     // Keep the scratch within a fixed budget: fewer resident waves for very large spp.
@@ -2636,8 +2719,11 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
     if (!c || !cam) return fail(RT_ERR_INVALID, "rt_render_async: NULL argument");
     if (spp == 0) return fail(RT_ERR_INVALID, "rt_render_async: spp == 0 (the reference panics: 0/0 in to_u8_array)");
     if (flags & ~RT_FLAG_ALL) return fail(RT_ERR_INVALID, "rt_render_async: unknown flag bits");
-    if ((flags & RT_FLAG_MODE_VECTORIZED) && (flags & RT_FLAG_MODE_SCALAR))
-        return fail(RT_ERR_INVALID, "rt_render_async: RT_FLAG_MODE_VECTORIZED and RT_FLAG_MODE_SCALAR are exclusive");
+    {
+        const uint32_t modes = flags & (RT_FLAG_MODE_VECTORIZED | RT_FLAG_MODE_SCALAR | RT_FLAG_MODE_VECTORIZED3);
+        if (modes & (modes - 1u))
+            return fail(RT_ERR_INVALID, "rt_render_async: the RT_FLAG_MODE_* flags are exclusive");
+    }
     if (spp > (1u << 20)) return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp > 2^20");
     if (cam->image_width == 0 || cam->image_height == 0) return fail(RT_ERR_INVALID, "rt_render_async: empty image");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "image too large");

@@ -1,7 +1,7 @@
 // rt-render — the reference's binary (src/main.rs:27-74) on the MI355X sample loop.
 //
 //   rt-render [--scene scene.toml] [--width 3840] [--height 2160] [--spp 100] [--bounces 50]
-//             [--seed 0x5EED0001] [--f32] [--root2] [--mode vectorized2|vectorized|scalar]
+//             [--seed 0x5EED0001] [--f32] [--root2] [--mode vectorized2|vectorized|vectorized3|scalar]
 //             [--out output.png|.ppm] [--dump-scene]
 //
 // --mode picks which of the reference's renderers is reproduced (include/rt_mi355x.h): the live
@@ -85,8 +85,9 @@ int main(int argc, char** argv) {
         else if (a == "--root2") flags |= RT_FLAG_ROOT2;
         else if (a == "--mode") {
             const std::string m = next();
-            flags &= ~(RT_FLAG_MODE_VECTORIZED | RT_FLAG_MODE_SCALAR);
+            flags &= ~(RT_FLAG_MODE_VECTORIZED | RT_FLAG_MODE_SCALAR | RT_FLAG_MODE_VECTORIZED3);
             if (m == "vectorized") flags |= RT_FLAG_MODE_VECTORIZED;
+            else if (m == "vectorized3") flags |= RT_FLAG_MODE_VECTORIZED3;
             else if (m == "scalar") flags |= RT_FLAG_MODE_SCALAR;
             else if (m != "vectorized2") { std::fprintf(stderr, "unknown mode %s\n", m.c_str()); return 2; }
         }
@@ -94,7 +95,7 @@ int main(int argc, char** argv) {
         else if (a == "--dump-scene") dump = true;
         else if (a == "-h" || a == "--help") {
             std::puts("rt-render [--scene scene.toml] [--width W] [--height H] [--spp S] [--bounces B] [--seed N] "
-                      "[--f32] [--root2] [--mode vectorized2|vectorized|scalar] [--out output.png] [--dump-scene]");
+                      "[--f32] [--root2] [--mode vectorized2|vectorized|vectorized3|scalar] [--out output.png] [--dump-scene]");
             return 0;
         } else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }

@@ -24,7 +24,8 @@ RT_FLAG_F32 = 0x1
 RT_FLAG_ROOT2 = 0x2
 RT_FLAG_MODE_VECTORIZED = 0x4   # render_vectorized -> trace_vectorized semantics
 RT_FLAG_MODE_SCALAR = 0x8       # render -> trace_rays semantics
-RT_FLAG_ALL = 0xF
+RT_FLAG_MODE_VECTORIZED3 = 0x10  # render_vectorized3 -> trace_vectorized3 semantics
+RT_FLAG_ALL = 0x1F
 
 
 class RtMaterial(ctypes.Structure):

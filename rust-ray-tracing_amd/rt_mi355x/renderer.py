@@ -49,10 +49,12 @@ class GpuRenderer(Renderer):
     seed: 64-bit key of the counter-based RNG (the reference's thread_rng is unseedable);
     precision: "f64" (reference arithmetic) or "f32"; root2: quirk Q1 off;
     mode: which reference renderer to reproduce — "vectorized2" (the live render_vectorized2,
-    default), "vectorized" (render_vectorized) or "scalar" (render); see include/rt_mi355x.h.
+    default), "vectorized" (render_vectorized), "vectorized3" (render_vectorized3) or "scalar" (render);
+    see include/rt_mi355x.h.
     """
 
-    MODES = {"vectorized2": 0, "vectorized": abi.RT_FLAG_MODE_VECTORIZED, "scalar": abi.RT_FLAG_MODE_SCALAR}
+    MODES = {"vectorized2": 0, "vectorized": abi.RT_FLAG_MODE_VECTORIZED, "vectorized3": abi.RT_FLAG_MODE_VECTORIZED3,
+             "scalar": abi.RT_FLAG_MODE_SCALAR}
 
     def __init__(self, device=0, seed=0x5EED0001, precision="f64", root2=False, mode="vectorized2", lib=None):
         if mode not in self.MODES:

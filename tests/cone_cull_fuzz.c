@@ -26,6 +26,7 @@ static float jitter(float r) {
 }
 static float rsq(float x) { return jitter(1.0f / sqrtf(x)); }
 static float rcp(float x) { return jitter(1.0f / x); }
+static float vsqrt(float x) { return jitter(sqrtf(x)); }   // v_sqrt_f32 (1 ulp)
 static float fbits(uint32_t b) { float x; memcpy(&x, &b, 4); return x; }
 
 // Does any of the three reference tests find a valid root?  (T = float)
@@ -143,12 +144,12 @@ int main(int argc, char** argv) {
             if (!(dt > 0.5f)) all = 1;
             if (bits(s2) > sm) sm = bits(s2);
         }
-        const float Sn = fmaf(sqrtf(fbits(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f);
+        const float Sn = fmaf(vsqrt(fbits(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f);
         if (!(Sn < 0.5f)) all = 1;
-        const float Cc = sqrtf(fmaf(-Sn, Sn, 1.0f));
+        const float Cc = vsqrt(fmaf(-Sn, Sn, 1.0f));
         const float t = fmaf(wz, az, fmaf(wy, ay, wx * ax));
         const float qx = fmaf(wy, az, -(wz * ay)), qy = fmaf(wz, ax, -(wx * az)), qz = fmaf(wx, ay, -(wy * ax));
-        const float pp = sqrtf(fmaf(qz, qz, fmaf(qy, qy, qx * qx)));
+        const float pp = vsqrt(fmaf(qz, qz, fmaf(qy, qy, qx * qx)));
         const float f = fmaf(pp, Cc, -(t * Sn));
         const int pass = all || !(f > rp);
         // the sphere's cluster (set_scene's bounds + build_cam_table's record): the target plus up to
@@ -179,7 +180,7 @@ int main(int argc, char** argv) {
         const float Wf[3] = {(float)Wx, (float)Wy, (float)Wz};
         const float tk = fmaf(Wf[2], az, fmaf(Wf[1], ay, Wf[0] * ax));
         const float kx = fmaf(Wf[1], az, -(Wf[2] * ay)), ky = fmaf(Wf[2], ax, -(Wf[0] * az)), kz = fmaf(Wf[0], ay, -(Wf[1] * ax));
-        const float pk = sqrtf(fmaf(kz, kz, fmaf(ky, ky, kx * kx)));
+        const float pk = vsqrt(fmaf(kz, kz, fmaf(ky, ky, kx * kx)));
         const int pass_k = all || !(fmaf(pk, Cc, -(tk * Sn)) > rpk);
         if (pass && !pass_k) ++cmiss;
         batches_all += all;

@@ -126,6 +126,7 @@ def test_header_constants_match_python_mirror():
     import re
     hdr = open(os.path.join(REPO, "include", "rt_mi355x.h")).read()
     defs = dict(re.findall(r"#define\s+(RT_[A-Z0-9_]+)\s+(0x[0-9A-Fa-f]+|\d+)u?\b", hdr))
-    assert {"RT_FLAG_F32", "RT_FLAG_ROOT2", "RT_FLAG_MODE_VECTORIZED", "RT_FLAG_MODE_SCALAR", "RT_FLAG_ALL"} <= set(defs)
+    assert {"RT_FLAG_F32", "RT_FLAG_ROOT2", "RT_FLAG_MODE_VECTORIZED", "RT_FLAG_MODE_SCALAR", "RT_FLAG_MODE_VECTORIZED3",
+            "RT_FLAG_ALL"} <= set(defs)
     for name, val in defs.items():
         assert getattr(abi, name) == int(val, 0), name

@@ -87,7 +87,8 @@ def test_cone_margin_constant_matches_kernel():
     expr = "sqrt((double)r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30"   # 64 u, 32 u
     assert expr in src
     assert expr.replace("(double)r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
-    assert "__builtin_fmaf(sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f)" in src
+    assert "__builtin_fmaf(__builtin_amdgcn_sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f)" in src
+    assert "__builtin_amdgcn_sqrtf(__builtin_fmaf(pz, pz" in src   # p by v_sqrt_f32; the fuzz models +-1 ulp
     # cluster records: rp_k >= rp_i + |c_i - C| for every member (the fuzz also checks this directly)
     assert "rup(R * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (wn + R) + 1e-30)" in src
     assert "RR * (1.0 + 0x1.0p-20) + (0x1.0p-9 + 0x1.0p-16) * (Wn + RR) + 1e-30" in \

@@ -294,7 +294,8 @@ def test_config_e_scene(renderer, flags, spp):
 
 
 # ---- semantics modes (tests/test_modes.py pins them on the CPU) ----
-MODES = [abi.RT_FLAG_MODE_VECTORIZED, abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_ROOT2, abi.RT_FLAG_MODE_SCALAR]
+MODES = [abi.RT_FLAG_MODE_VECTORIZED, abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_ROOT2, abi.RT_FLAG_MODE_SCALAR,
+         abi.RT_FLAG_MODE_VECTORIZED3, abi.RT_FLAG_MODE_VECTORIZED3 | abi.RT_FLAG_ROOT2]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -310,14 +311,16 @@ def test_modes_scene_100(renderer, scene_100, mode, spp, depth, prec):
     assert_parity(renderer, scene_100, cam_for(24, 14), depth, spp, mode | prec)
 
 
-@pytest.mark.parametrize("flags", [abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_MODE_SCALAR, 0x10, 0x80000000])
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_MODE_SCALAR,
+                                   abi.RT_FLAG_MODE_VECTORIZED3 | abi.RT_FLAG_MODE_VECTORIZED, 0x20, 0x80000000])
 def test_invalid_flag_bits(renderer, scene_a, flags):
     with pytest.raises(abi.RtError) as e:
         gpu(renderer, scene_a, cam_for(8, 4), 8, 4, flags=flags)
     assert e.value.code == abi.RT_ERR_INVALID
 
 
-@pytest.mark.parametrize("mode,flag", [("scalar", abi.RT_FLAG_MODE_SCALAR), ("vectorized", abi.RT_FLAG_MODE_VECTORIZED)])
+@pytest.mark.parametrize("mode,flag", [("scalar", abi.RT_FLAG_MODE_SCALAR), ("vectorized", abi.RT_FLAG_MODE_VECTORIZED),
+                                       ("vectorized3", abi.RT_FLAG_MODE_VECTORIZED3)])
 def test_cli_modes(tmp_path, mode, flag):
     """rt-render --mode: the PPM bytes equal the oracle's image in that mode."""
     import subprocess

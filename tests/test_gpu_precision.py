@@ -187,3 +187,32 @@ def test_config_e_filter_off_same_image(renderer, monkeypatch, flags):
     _, lin_off, st_off = render(renderer, flat, cam, 50, 32, flags)
     np.testing.assert_array_equal(lin_off, lin_o)
     assert st_off.box_groups > st_on.box_groups and st_off.filter_groups > st_on.filter_groups
+
+
+# ---------------------------------------------------------------- vectorized3 (render_vectorized3)
+@pytest.mark.parametrize("spp,prec", [(512, 0), (100, abi.RT_FLAG_F32), (1024, abi.RT_FLAG_F32), (130, 0)])
+def test_vectorized3_large_spp(renderer, spp, prec):
+    """trace_vectorized3's swap partition replayed over many 64-slot passes (P up to 1024), bit-exact
+    against the oracle's literal two-pointer loop (ray_tracing.rs:561-607)."""
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = cam_for(12, 7)
+    rgb, lin, st = render(renderer, flat, cam, 50, spp, abi.RT_FLAG_MODE_VECTORIZED3 | prec)
+    rgb_o, lin_o, segs_o, _ = oracle_render(flat, cam, 50, spp, SEED, abi.RT_FLAG_MODE_VECTORIZED3,
+                                            precision="f32" if prec else "f64")
+    np.testing.assert_array_equal(lin, lin_o)
+    np.testing.assert_array_equal(rgb, rgb_o)
+    assert st.ray_segments == segs_o
+
+
+@pytest.mark.parametrize("depth", [60, 200])
+def test_vectorized3_long_paths(renderer, depth):
+    """Camera inside a glass sphere with root2 allowed: some rays stay trapped for all `depth` bounces,
+    so the partition is replayed for up to 200 bounces with survivors in the active chunks."""
+    flat = rt.FlatScene(np.array([[16.0, 2.0, 56.5]]), np.array([40.0]), np.array([0], np.uint32),
+                        [rt.Dielectric(1.5, False)])
+    cam = cam_for(16, 9)
+    flags = abi.RT_FLAG_MODE_VECTORIZED3 | abi.RT_FLAG_ROOT2
+    _, lin, st = render(renderer, flat, cam, depth, 24, flags)
+    _, lin_o, segs_o, _ = oracle_render(flat, cam, depth, 24, SEED, flags)
+    np.testing.assert_array_equal(lin, lin_o)
+    assert st.ray_segments == segs_o
