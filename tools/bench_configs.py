@@ -32,7 +32,9 @@ def run(config, precision, stride):
     return {"config": config, "precision": precision, "rows": f"every {stride} row(s)", "pixels": tile.row_count * W,
             "spp": spp, "spheres": n_sph, "kernel_ms": round(st.kernel_ms, 2),
             "msamples_per_s_per_gpu": round(samples / (st.kernel_ms / 1e3) / 1e6, 1),
-            "tflops_per_gpu": round(17 * n_sph * st.ray_segments / (st.kernel_ms / 1e3) / 1e12, 2),
+            "brute_force_equiv_tflops": round(17 * n_sph * st.ray_segments / (st.kernel_ms / 1e3) / 1e12, 2),
+            "roofline_frac": round(sum(f / (pk * 1e12) for f, pk in zip(abi.executed_flop(st, precision), (157.3, 78.6)))
+                                   / (st.kernel_ms / 1e3), 4),
             "segments_per_sample": round(st.ray_segments / samples, 4),
             "lane_utilisation": round(st.ray_segments / max(1, st.lane_slots), 4), "wall_s": round(wall, 2)}
 
