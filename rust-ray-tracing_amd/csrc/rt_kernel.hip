@@ -135,6 +135,10 @@ template <typename T> struct KParams {
     const float* fsup;         // super boxes (4 clusters each), 4 per group
     const float* fmeg;         // mega boxes (4 supers each), 4 per group; n_mg groups, 0: no mega level
     uint32_t n_mg;
+    // MEGA kernels: the sphere filter in cluster-local frames (pack_local): filter groups with centres
+    // relative to their cluster's centre, and per cluster {Cx, Cy, Cz, Rc, r2max, 1/r2min, 0, 0}
+    const float* lfsph;
+    const float* lclu;
     const uint32_t* ridx;
     uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
@@ -599,7 +603,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // The filter constants need no correctly rounded division or square root: v_rsq_f32 and
         // v_rcp_f32 (1 ulp) add a few u to the basis error, well inside the margin (the fuzz tests
         // model them as +-1 ulp).  1/r2min, 0.5/r2min and 8u/sqrt(r2min) come from the host.
-        const float sg = __builtin_amdgcn_rsqf(__builtin_fmaf(m, qa.f_ir2, 1.0f));
+        // MEGA: the basis stays unscaled here; each walked cluster scales it by its own local margin.
+        const float sg = MEGA ? 1.0f : __builtin_amdgcn_rsqf(__builtin_fmaf(m, qa.f_ir2, 1.0f));
         const float s1 = __builtin_amdgcn_rsqf(L) * sg, s2 = __builtin_amdgcn_rsqf(L * af) * sg;
         float e1x = fdz * s1, e1z = -fdx * s1;
         float e2x = -(fdx * fdy) * s2, e2y = L * s2, e2z = -(fdy * fdz) * s2;
@@ -720,15 +725,41 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             ++n_box;
             uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
             while (mask != 0u) {
-                const uint32_t g0 = nxg + 4u * (4u * sup + (uint32_t)__builtin_ctz(mask));
+                const uint32_t kc = 4u * sup + (uint32_t)__builtin_ctz(mask);   // cluster
+                const uint32_t g0 = nxg + 4u * kc;
                 mask &= mask - 1u;
                 KSTAT(4);
                 n_filt += 4u;
-                sphere_loop(ff + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
+                f2 L0 = K0, L1 = K1, L2 = K2, L3 = K3;
+                cptr<float> fg = ff;
+                if constexpr (MEGA) {
+                    // The cluster's frame (pack_local): o' = o - C_k (fp64 rays: in double, then
+                    // rounded), the margin from |o'|_1 and the cluster's Rc, r2max and 1/r2min, the
+                    // basis scaled by it, and o' projected on the scaled basis.
+                    const auto& ql = *cold_args<T>();
+                    cptr<float> lr = (cptr<float>)__builtin_assume_aligned(ql.lclu, 32);
+                    const float Ckx = lr[8u * kc], Cky = lr[8u * kc + 1u], Ckz = lr[8u * kc + 2u];
+                    const float Rc = lr[8u * kc + 3u], r2x = lr[8u * kc + 4u], ir2 = lr[8u * kc + 5u];
+                    float opx, opy, opz;
+                    if constexpr (sizeof(T) == 4) {
+                        opx = o.x - Ckx; opy = o.y - Cky; opz = o.z - Ckz;
+                    } else {
+                        opx = (float)(o.x - (double)Ckx); opy = (float)(o.y - (double)Cky); opz = (float)(o.z - (double)Ckz);
+                    }
+                    const float pmk = ((fabsf(opx) + fabsf(opy)) + fabsf(opz)) + Rc;
+                    const float mk = kFilterMargin * __builtin_fmaf(pmk, pmk, r2x);
+                    const float sgk = __builtin_amdgcn_rsqf(__builtin_fmaf(mk, ir2, 1.0f));
+                    L0 = K0 * sgk; L1 = K1 * sgk; L2 = K2 * sgk;
+                    const float oe1l = __builtin_fmaf(opz, L0.y, opx * L0.x);
+                    const float oe2l = __builtin_fmaf(opz, L2.x, __builtin_fmaf(opy, L1.y, opx * L1.x));
+                    L3 = f2{-oe1l, -oe2l};
+                    fg = (cptr<float>)__builtin_assume_aligned(ql.lfsph, 64);
+                }
+                sphere_loop(fg + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                     uint32_t s0, s1;
                     // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
                     // rejects them as well (the filter passes every sphere the reference can hit).
-                    if (__ballot(is_cand(filter_group(cur, K0, K1, K2, K3, s0, s1))) != 0ull) {
+                    if (__ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1))) != 0ull) {
                         // only the sphere pairs some lane passes (one compare each, taken groups only)
                         uint32_t pairs = 3u;
 #ifndef RT_EXP_PAIRS_F64
@@ -2010,6 +2041,8 @@ struct rt_context {
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
     void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
     void* meg64 = nullptr; void* meg32 = nullptr;   // mega boxes (4 supers each; big scenes only)
+    void* lfs64 = nullptr; void* lfs32 = nullptr;   // cluster-local filter groups (big scenes only)
+    void* lcl64 = nullptr; void* lcl32 = nullptr;   // ... and the per-cluster frame records
     uint32_t n_mg = 0;
     uint32_t* ridx = nullptr;
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
@@ -2106,6 +2139,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->sup64); (void)hipFree(c->sup32);
     c->sup64 = c->sup32 = nullptr;
     (void)hipFree(c->meg64); (void)hipFree(c->meg32);
+    (void)hipFree(c->lfs64); (void)hipFree(c->lfs32); (void)hipFree(c->lcl64); (void)hipFree(c->lcl32);
+    c->lfs64 = c->lfs32 = c->lcl64 = c->lcl32 = nullptr;
     c->meg64 = c->meg32 = nullptr;
     c->n_mg = 0;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
@@ -2417,6 +2452,56 @@ static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec
     (void)r2max;
 }
 
+// Cluster-local filter records for the MEGA kernels (nearest_hit).  Far from the origin the scene-wide
+// margin of the sphere filter, 48 u ((max|c|_1 + |o|_1)^2 + max r2f), grows with the coordinates'
+// magnitudes (config E: ~0.06 against r^2 = 0.04), though the rounding it covers grows with the
+// distances involved.  In a frame centred on the cluster (C_k: its box centre, an fp32 value) the
+// filter sees c' = RN_f(c - C_k) and o' = o - C_k, and the same margin formula with |c'|_1 <= Rc_k and
+// |o'|_1 in place of the scene-wide magnitudes bounds the same errors (tests/filter_margin_fuzz.c,
+// local mode).  r2f is floored per cluster at 2^-10 of its largest (a tiny sphere cannot inflate the
+// others by more than that ratio).  Slot order and group layout as the scene-wide filter stream;
+// always-exact slots get dummies (they are never filtered).
+template <typename T>
+static void pack_local(const std::vector<T>& cen, const SweepLayout& L, const std::vector<float>& top,
+                       std::vector<float>& lfgrp, std::vector<float>& lrec) {
+    auto up32 = [](double v) -> float {
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+        return f;
+    };
+    const size_t ns = L.slot.size(), nc = L.members.size();
+    lfgrp.assign((size_t)16 * (ns / 4 + 1), 0.0f);
+    for (size_t i = 0; i < ns + 4; ++i) lfgrp[(size_t)16 * (i / 4) + 8 * ((i % 4) / 2) + 6 + (i % 2)] = -INFINITY;
+    lrec.assign((size_t)8 * (nc ? nc : 1), 0.0f);
+    for (size_t k = 0; k < nc; ++k) {
+        const auto& m = L.members[k];
+        if (m.empty()) continue;
+        float Ck[3];
+        for (int f = 0; f < 3; ++f) Ck[f] = top[kBoxFloats * (k / 4) + 12 * ((k % 4) / 2) + 2 * f + (k % 2)];
+        double r2max = 0.0, rc = 0.0;
+        for (uint32_t i : m) r2max = std::max(r2max, (double)(cen[4 * i + 3] * cen[4 * i + 3]));   // r.powi(2) in T
+        const double floor2 = r2max * 0x1.0p-10;
+        double r2min = INFINITY, r2fmax = 0.0;
+        for (uint32_t j = 0; j < m.size(); ++j) {
+            const uint32_t i = m[j];
+            const size_t slot = (size_t)4 * L.n_xg + kClusterMax * k + j;   // members in cluster-slot order
+            float f[4];
+            for (int a = 0; a < 3; ++a) f[a] = (float)((double)cen[4 * i + a] - (double)Ck[a]);   // RN_f(c - C_k)
+            const T r2 = cen[4 * i + 3] * cen[4 * i + 3];
+            f[3] = up32(std::max((double)r2, floor2));
+            rc = std::max(rc, std::fabs((double)f[0]) + std::fabs((double)f[1]) + std::fabs((double)f[2]));
+            r2min = std::min(r2min, (double)f[3]);
+            r2fmax = std::max(r2fmax, (double)f[3]);
+            for (int q = 0; q < 4; ++q) lfgrp[(size_t)16 * (slot / 4) + 8 * ((slot % 4) / 2) + 2 * q + (slot % 2)] = f[q];
+        }
+        float* r = &lrec[8 * k];
+        r[0] = Ck[0]; r[1] = Ck[1]; r[2] = Ck[2];
+        r[3] = up32(rc);
+        r[4] = up32(r2fmax);
+        r[5] = up32(1.0 / r2min);
+    }
+}
+
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     if (!c || !s) return fail(RT_ERR_INVALID, "rt_context_set_scene: NULL argument");
     if (s->n_spheres && (!s->center || !s->radius || !s->material || !s->materials))
@@ -2461,6 +2546,13 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if (c->n_mg) {
             if ((rc = up(&c->meg64, m64.data(), m64.size() * sizeof(float))) != RT_OK) return rc;
             if ((rc = up(&c->meg32, m32.data(), m32.size() * sizeof(float))) != RT_OK) return rc;
+            std::vector<float> lf64, lf32, lr64, lr32;
+            pack_local(c64, L, t64, lf64, lr64);
+            pack_local(c32, L, t32, lf32, lr32);
+            if ((rc = up(&c->lfs64, lf64.data(), lf64.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->lfs32, lf32.data(), lf32.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->lcl64, lr64.data(), lr64.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->lcl32, lr32.data(), lr32.size() * sizeof(float))) != RT_OK) return rc;
         }
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
@@ -2587,6 +2679,8 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.fsup = (const float*)(f64 ? c->sup64 : c->sup32);
     p.fmeg = (const float*)(f64 ? c->meg64 : c->meg32);
     p.n_mg = c->n_mg;
+    p.lfsph = (const float*)(f64 ? c->lfs64 : c->lfs32);
+    p.lclu = (const float*)(f64 ? c->lcl64 : c->lcl32);
     p.ridx = c->ridx;
     p.n_top = c->n_top;
     p.n_xg = c->n_xg;

@@ -9,7 +9,11 @@
 // The reference formulas are objects.rs:252-257 (hit_packed, FMA where it writes mul_add) and
 // objects.rs:217-222 (Sphere::hit, no FMA).
 // mode 0: fp32 hit_packed; 1: fp32 scalar Sphere::hit; 2: fp64 hit_packed; 3: fp64 scalar.
-// Usage: filter_margin_fuzz N MODE [SEED] -> prints misses and the worst margin needed, in u.
+// LOCAL = 1: the MEGA kernels' cluster-local frame (pack_local + nearest_hit): the whole case is moved
+// far from the origin (up to 1000x its size), a cluster centre Ck (fp32) is put 1..100 radii from the
+// sphere, and the filter sees c' = RN_f(c - Ck), o' = o - Ck (fp64 rays: in double, then rounded) with
+// the margin 48 u ((|c'|_1 + |o'|_1)^2 + r2f): the same formula in local magnitudes.
+// Usage: filter_margin_fuzz N MODE [SEED] [LOCAL] -> prints misses and the worst margin needed, in u.
 #include <math.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -31,6 +35,7 @@ int main(int argc, char** argv) {
     const long n = argc > 1 ? atol(argv[1]) : 10000000;
     const int mode = argc > 2 ? atoi(argv[2]) : 0;
     if (argc > 3) s = strtoull(argv[3], 0, 0) | 1;
+    const int local = argc > 4 ? atoi(argv[4]) : 0;
     long acc = 0, miss = 0; double worst = 0;
     for (long it = 0; it < n; ++it) {
         double S = pow(10.0, -1 + 4 * U());
@@ -51,6 +56,17 @@ int main(int argc, char** argv) {
         double rho = r * (1 + (U() - 0.5) * 1e-3 * pow(10.0, -6 * U()));
         double C[3];
         for (int k = 0; k < 3; ++k) C[k] = O[k] + tpar * D[k] / sqrt(a0) + px[k] / pl * rho;
+        float Ck[3] = {0, 0, 0};
+        if (local) {   // far from the origin; a cluster centre near the sphere
+            const double tm = S * pow(10.0, 3 * U());
+            const double g = r * pow(10.0, 2 * U());
+            for (int k = 0; k < 3; ++k) {
+                const double t = N() * tm;
+                O[k] += t; C[k] += t;
+                Ck[k] = (float)(C[k] + N() * g);
+            }
+            if (mode < 2) for (int k = 0; k < 3; ++k) O[k] = (float)O[k];
+        }
         if (mode < 2) for (int k = 0; k < 3; ++k) C[k] = (float)C[k];
         int ref_ok;
         float r2f;
@@ -99,6 +115,13 @@ int main(int argc, char** argv) {
         // the kernel's m uses the scene-wide max |c|_1 and max r2f, and its r2min is the scene's
         // smallest r2f; this sphere's own values bound those from the unfavourable side, so the
         // inflation tested here (r2f * (1 + m / r2f) = r2f + m) is never larger than the kernel's
+        if (local) {   // pack_local's c' and the kernel's o'
+            cx = (float)((double)C[0] - (double)Ck[0]); cy = (float)((double)C[1] - (double)Ck[1]);
+            cz = (float)((double)C[2] - (double)Ck[2]);
+            if (mode < 2) { fox = fox - Ck[0]; foy = foy - Ck[1]; foz = foz - Ck[2]; }
+            else { fox = (float)(O[0] - (double)Ck[0]); foy = (float)(O[1] - (double)Ck[1]); foz = (float)(O[2] - (double)Ck[2]); }
+            on = ((fabsf(fox) + fabsf(foy)) + fabsf(foz));
+        }
         float cmax = fabsf(cx) + fabsf(cy) + fabsf(cz);
         float pm = cmax + on;
         float m = KM * fmaf(pm, pm, r2f);

@@ -32,10 +32,13 @@ def test_margin_constant_matches_kernel():
     assert "KM = 48.0f * 0x1.0p-24f" in open(os.path.join(HERE, "filter_margin_fuzz.c")).read()
 
 
+@pytest.mark.parametrize("local", [0, 1], ids=["scene", "cluster_local"])
 @pytest.mark.parametrize("mode", [0, 1, 2, 3], ids=["f32_packed", "f32_scalar", "f64_packed", "f64_scalar"])
-def test_filter_is_conservative(fuzz_bin, mode):
-    r = subprocess.run([fuzz_bin, "3000000", str(mode), str(0x9E3779B97F4A7C15 + mode)], capture_output=True,
-                       text=True, timeout=300)
+def test_filter_is_conservative(fuzz_bin, mode, local):
+    """The sphere filter passes every sphere the reference's arithmetic could hit, in the scene-wide
+    frame and (local) in the MEGA kernels' cluster-local frames far from the origin."""
+    r = subprocess.run([fuzz_bin, "3000000", str(mode), str(0x9E3779B97F4A7C15 + mode + 17 * local), str(local)],
+                       capture_output=True, text=True, timeout=300)
     line = r.stdout.strip()
     fields = line.split()
     misses = int(fields[fields.index("misses") + 1])
