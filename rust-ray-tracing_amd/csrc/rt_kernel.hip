@@ -139,6 +139,10 @@ template <typename T> struct KParams {
     // relative to their cluster's centre, and per cluster {Cx, Cy, Cz, Rc, r2max, 1/r2min, 0, 0}
     const float* lfsph;
     const float* lclu;
+    const float* lclb;         // ... the box levels in group-local frames (pack_local_boxes): per super its
+    const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
+    const float* lmeg;
+    float l_r2max, l_hir2, l_isr;   // their margin constants: max local r2f, 0.5 / min, 8 u / sqrt(min)
     const uint32_t* ridx;
     uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
@@ -236,6 +240,36 @@ __device__ __forceinline__ void box_loop(cptr<float> f, uint32_t ng, F&& group) 
         __builtin_amdgcn_s_waitcnt(0xC07F);
         __builtin_amdgcn_sched_barrier(0);
         A = load_box(f, g + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        group(B, g + 1);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (g < ng) group(A, g);
+}
+
+// A box group in a group-local frame (MEGA kernels, pack_local_boxes): 24 floats of boxes (BoxGroup
+// layout), then the frame {Sx, Sy, Sz, Rg}, padded to 128 bytes (two s_load_dwordx16).
+struct alignas(64) LBoxGroup { float v[32]; };
+__device__ __forceinline__ LBoxGroup load_lbox(const __attribute__((address_space(4))) float* f, uint32_t g) {
+    LBoxGroup r;
+#pragma unroll
+    for (uint32_t e = 0; e < 28; ++e) r.v[e] = f[g * 32u + e];
+    return r;
+}
+template <typename F>
+__device__ __forceinline__ void lbox_loop(cptr<float> f, uint32_t ng, F&& group) {
+    LBoxGroup A = load_lbox(f, 0);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t g = 0;
+    for (; g + 1 < ng; g += 2) {
+        const LBoxGroup B = load_lbox(f, g + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        group(A, g);
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        __builtin_amdgcn_sched_barrier(0);
+        A = load_lbox(f, g + 2);
         __builtin_amdgcn_sched_barrier(0);
         group(B, g + 1);
         __builtin_amdgcn_s_waitcnt(0xC07F);
@@ -381,6 +415,9 @@ __device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2
                                           pass(nx.y, ny.y, nz.y, ux.y, uy.y, uz.y, std::integral_constant<uint32_t, 2>{}));
 }
 __device__ __forceinline__ uint32_t box_mask(const BoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
+    return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
+}
+__device__ __forceinline__ uint32_t box_mask(const LBoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
     return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
 }
 
@@ -634,6 +671,24 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // op's op_sel (filter_group), so the filter state is 8 VGPRs, not 16.
         const f2 K0 = {e1x, e1z}, K1 = {e2x, e2y}, K2 = {e2z, 0.0f}, K3 = {-oe1, -oe2};
         const f2 B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, 0.0f};
+        // MEGA: a box group in its own frame S (pack_local_boxes): o' = o - S (fp64 rays: in double,
+        // then rounded), the margin from pm = |o'|_1 + Rg, A = -o'.i, J = |i| (1 + kappa).
+        auto lmask = [&](const LBoxGroup& g) -> uint32_t {
+            const auto& ql = *cold_args<T>();
+            const float Sx = g.v[24], Sy = g.v[25], Sz = g.v[26], Rg = g.v[27];
+            float opx, opy, opz;
+            if constexpr (sizeof(T) == 4) {
+                opx = o.x - Sx; opy = o.y - Sy; opz = o.z - Sz;
+            } else {
+                opx = (float)(o.x - (double)Sx); opy = (float)(o.y - (double)Sy); opz = (float)(o.z - (double)Sz);
+            }
+            const float pmg = ((fabsf(opx) + fabsf(opy)) + fabsf(opz)) + Rg;
+            const float mg = kFilterMargin * __builtin_fmaf(pmg, pmg, ql.l_r2max);
+            const float kp = 1.0f + __builtin_fmaf(mg, ql.l_hir2, pmg * ql.l_isr);
+            const f2 C1 = {iz, -(opz * iz)}, C2 = {-(opx * ix), -(opy * iy)};
+            const f2 C3 = {fabsf(ix) * kp, fabsf(iy) * kp}, C4 = {fabsf(iz) * kp, 0.0f};
+            return box_mask(g, B0, C1, C2, C3, C4);
+        };
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
         // the sphere pairs set in `pairs` (bit q: spheres 4g+2q, 4g+2q+1; wave-uniform).
         auto exact4 = [&](uint32_t g, uint32_t pairs = 3u) {
@@ -723,7 +778,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         auto walk_super = [&](uint32_t sup) {
             KSTAT(5);
             ++n_box;
-            uint32_t mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
+            uint32_t mask;
+            if constexpr (MEGA) mask = lmask(load_lbox((cptr<float>)__builtin_assume_aligned(qa.lclb, 64), sup));
+            else mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
             while (mask != 0u) {
                 const uint32_t kc = 4u * sup + (uint32_t)__builtin_ctz(mask);   // cluster
                 const uint32_t g0 = nxg + 4u * kc;
@@ -775,32 +832,47 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         };
         // The top level is the super boxes, or (MEGA: scenes with more than 8 super groups, config E)
         // the mega boxes; chunks of 8 top groups (32 boxes) give a 32-bit wave mask of the passing
-        // top boxes.  A mega box nd covers super group nd.
-        cptr<float> fu = MEGA ? (cptr<float>)__builtin_assume_aligned(qa.fmeg, 32) : fs;
-        const uint32_t ntg = MEGA ? qa.n_mg : nsg, ntn = MEGA ? nsg : ntop;   // top groups, top boxes
-        for (uint32_t t0 = 0; t0 < ntg; t0 += 8u) {
-            uint32_t tmask = 0;
-            n_box += min(8u, ntg - t0);
-            box_loop(fu + kBoxFloats * t0, min(8u, ntg - t0), [&](const BoxGroup& cur, uint32_t t) {
-                KSTAT(5);
-                tmask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
-            });
-            while (tmask != 0u) {
-                const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);
-                tmask &= tmask - 1u;
-                // padding boxes past the last one are empty; a degenerate lane (all box times NaN)
-                // passes them, and nothing lies behind them
-                if (nd >= ntn) break;
-                if constexpr (MEGA) {
+        // top boxes.  A mega box nd covers super group nd.  MEGA kernels test every level in
+        // group-local frames (lmask).
+        if constexpr (MEGA) {
+            cptr<float> lm = (cptr<float>)__builtin_assume_aligned(qa.lmeg, 64);
+            cptr<float> ls = (cptr<float>)__builtin_assume_aligned(qa.lsup, 64);
+            const uint32_t ntg = qa.n_mg;
+            for (uint32_t t0 = 0; t0 < ntg; t0 += 8u) {
+                uint32_t tmask = 0;
+                n_box += min(8u, ntg - t0);
+                lbox_loop(lm + 32u * t0, min(8u, ntg - t0), [&](const LBoxGroup& cur, uint32_t t) {
+                    KSTAT(5);
+                    tmask |= lmask(cur) << (4u * t);
+                });
+                while (tmask != 0u) {
+                    const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);
+                    tmask &= tmask - 1u;
+                    if (nd >= nsg) break;   // padding megas (empty boxes; see below)
                     ++n_box;
-                    uint32_t smask = box_mask(load_box(fs, nd), B0, B1, B2, B3, B4);
+                    uint32_t smask = lmask(load_lbox(ls, nd));
                     while (smask != 0u) {
                         const uint32_t sup = 4u * nd + (uint32_t)__builtin_ctz(smask);
                         smask &= smask - 1u;
                         if (sup >= ntop) break;
                         walk_super(sup);
                     }
-                } else {
+                }
+            }
+        } else {
+            for (uint32_t t0 = 0; t0 < nsg; t0 += 8u) {
+                uint32_t tmask = 0;
+                n_box += min(8u, nsg - t0);
+                box_loop(fs + kBoxFloats * t0, min(8u, nsg - t0), [&](const BoxGroup& cur, uint32_t t) {
+                    KSTAT(5);
+                    tmask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
+                });
+                while (tmask != 0u) {
+                    const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);
+                    tmask &= tmask - 1u;
+                    // padding supers past the last one are empty boxes; a degenerate lane (all box
+                    // times NaN) passes them, and nothing lies behind them
+                    if (nd >= ntop) break;
                     walk_super(nd);
                 }
             }
@@ -1797,11 +1869,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                          const V3<T>& td) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
+#ifndef RT_EXP_NO_EWRITE   // traffic experiment only: results are wrong
             sc.set_e(t_slot, t_sid, e);
+#endif
             if (MODE == kModeV2) {
                 // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
                 // the copies into them raised the register peak (spills in the sphere sweeps)
+#ifndef RT_EXP_NO_CWRITE   // traffic experiment only: results are wrong
                 if (skyhit) sc.store_c(t_slot, t_sid, tc.x, tc.y, tc.z);
+#endif
             } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
                 V3<T> v = mk(T(0.0), T(0.0), T(0.0));
                 if (skyhit) { const V3<T> sk = sky(td.y); v = mk(tc.x * sk.x, tc.y * sk.y, tc.z * sk.z); }
@@ -1869,7 +1945,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const V3<T> vu = mk(q.vu[0], q.vu[1], q.vu[2]), vv = mk(q.vv[0], q.vv[1], q.vv[2]);
             const V3<T> pc = add(mk(q.ulc[0], q.ulc[1], q.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
             bd = unit(sub(pc, mk(q.center[0], q.center[1], q.center[2])));
+#ifndef RT_EXP_NO_YWRITE   // traffic experiment only: results are wrong
             if (MODE == kModeV2) wave_scratch<T>(wave).y(bslot, bsid) = bd.y;   // primary y (quirk Q2)
+#endif
         }
         T bt = T(0);
         int bi = -1;
@@ -1960,7 +2038,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (fresh) {
             k = 0;
             live = true;
+#ifndef RT_EXP_NO_YWRITE   // traffic experiment only: results are wrong
             if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
+#endif
         } else if (scat) {
             k += 1u;
         }
@@ -2043,6 +2123,8 @@ struct rt_context {
     void* meg64 = nullptr; void* meg32 = nullptr;   // mega boxes (4 supers each; big scenes only)
     void* lfs64 = nullptr; void* lfs32 = nullptr;   // cluster-local filter groups (big scenes only)
     void* lcl64 = nullptr; void* lcl32 = nullptr;   // ... and the per-cluster frame records
+    void* lbx64[3] = {}; void* lbx32[3] = {};       // local box levels: cluster boxes, supers, megas
+    float l_r2max64 = 0, l_r2min64 = 0, l_r2max32 = 0, l_r2min32 = 0;
     uint32_t n_mg = 0;
     uint32_t* ridx = nullptr;
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
@@ -2141,6 +2223,10 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->meg64); (void)hipFree(c->meg32);
     (void)hipFree(c->lfs64); (void)hipFree(c->lfs32); (void)hipFree(c->lcl64); (void)hipFree(c->lcl32);
     c->lfs64 = c->lfs32 = c->lcl64 = c->lcl32 = nullptr;
+    for (int lv = 0; lv < 3; ++lv) {
+        (void)hipFree(c->lbx64[lv]); (void)hipFree(c->lbx32[lv]);
+        c->lbx64[lv] = c->lbx32[lv] = nullptr;
+    }
     c->meg64 = c->meg32 = nullptr;
     c->n_mg = 0;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
@@ -2463,7 +2549,7 @@ static void pack_sweep(const std::vector<T>& cen, const std::vector<float>& frec
 // always-exact slots get dummies (they are never filtered).
 template <typename T>
 static void pack_local(const std::vector<T>& cen, const SweepLayout& L, const std::vector<float>& top,
-                       std::vector<float>& lfgrp, std::vector<float>& lrec) {
+                       std::vector<float>& lfgrp, std::vector<float>& lrec, std::vector<float>& r2l) {
     auto up32 = [](double v) -> float {
         float f = (float)v;
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
@@ -2489,6 +2575,8 @@ static void pack_local(const std::vector<T>& cen, const SweepLayout& L, const st
             for (int a = 0; a < 3; ++a) f[a] = (float)((double)cen[4 * i + a] - (double)Ck[a]);   // RN_f(c - C_k)
             const T r2 = cen[4 * i + 3] * cen[4 * i + 3];
             f[3] = up32(std::max((double)r2, floor2));
+            if (r2l.size() <= i) r2l.resize((size_t)i + 1, -INFINITY);
+            r2l[i] = f[3];
             rc = std::max(rc, std::fabs((double)f[0]) + std::fabs((double)f[1]) + std::fabs((double)f[2]));
             r2min = std::min(r2min, (double)f[3]);
             r2fmax = std::max(r2fmax, (double)f[3]);
@@ -2500,6 +2588,137 @@ static void pack_local(const std::vector<T>& cen, const SweepLayout& L, const st
         r[4] = up32(r2fmax);
         r[5] = up32(1.0 / r2min);
     }
+}
+
+// The MEGA kernels' box levels in group-local frames.  World boxes as pack_sweep builds them, but
+// around the spheres' locally floored radii (pack_local's r2f), so a far-from-origin scene keeps its
+// boxes tight: clusters, their union per super, the supers' union per mega.  Every box group is then
+// stored around its own frame S (the fp32 centre of its boxes' union): 24 floats of boxes with
+// C' = RN_f(C - S) and H widened by 2^-22 |C'|, then {S, Rg = max |C'|_1 + |H'|_1} (LBoxGroup); the
+// lane tests it with o' = o - S and the margin from |o'|_1 + Rg (nearest_hit; tests/box_cull_fuzz.c,
+// local mode).  One empty group past the end of each level (prefetch target).
+constexpr uint32_t kLBoxFloats = 32;
+template <typename T>
+static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, const std::vector<float>& r2l,
+                             std::vector<float>& lclb, std::vector<float>& lsup, std::vector<float>& lmeg,
+                             float& r2max, float& r2min) {
+    auto up32 = [](double v) -> float {
+        float f = (float)v;
+        if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+        return f;
+    };
+    const size_t nc = L.members.size();
+    // world boxes, BoxGroup layout (4 per 24 floats), like pack_sweep's, around sqrt(local r2f)
+    auto put = [](std::vector<float>& v, size_t k, const float b[6]) {
+        const size_t tg = k / 4, j = k % 4;
+        for (int f = 0; f < 6; ++f) v[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)] = b[f];
+    };
+    auto get = [](const std::vector<float>& v, size_t k, float b[6]) {
+        const size_t tg = k / 4, j = k % 4;
+        for (int f = 0; f < 6; ++f) b[f] = v[kBoxFloats * tg + 12 * (j / 2) + 2 * f + (j % 2)];
+    };
+    auto box_of = [&](double lo[3], double hi[3], bool inf, float b[6]) {
+        for (int a = 0; a < 3; ++a) {
+            b[a] = inf ? 0.0f : (float)(0.5 * (lo[a] + hi[a]));
+            const double h = std::max(hi[a] - (double)b[a], (double)b[a] - lo[a]);
+            b[3 + a] = inf ? INFINITY : up32(h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a]));
+        }
+    };
+    const float kEmpty[6] = {0.0f, 0.0f, 0.0f, -INFINITY, -INFINITY, -INFINITY};
+    std::vector<float> wcl((size_t)kBoxFloats * ((nc + 3) / 4 + 1));
+    for (size_t k = 0; k < 4 * (wcl.size() / kBoxFloats); ++k) put(wcl, k, kEmpty);
+    double rmax = 0.0, rmin = INFINITY;
+    for (size_t k = 0; k < nc; ++k) {
+        if (L.members[k].empty()) continue;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool inf = false;
+        for (uint32_t i : L.members[k]) {
+            if (!(r2l[i] < INFINITY)) inf = true;
+            rmax = std::max(rmax, (double)r2l[i]);
+            rmin = std::min(rmin, (double)r2l[i]);
+            const double r = std::sqrt((double)r2l[i]);
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], (double)(float)cen[4 * i + a] - r);
+                hi[a] = std::max(hi[a], (double)(float)cen[4 * i + a] + r);
+            }
+        }
+        float b[6];
+        box_of(lo, hi, inf, b);
+        put(wcl, k, b);
+    }
+    r2max = up32(rmax);
+    r2min = std::isfinite(rmin) ? (float)rmin : 0.0f;
+    auto unite = [&](const std::vector<float>& lower, size_t nup, std::vector<float>& upper) {
+        upper.assign((size_t)kBoxFloats * ((nup + 3) / 4 + 1), 0.0f);
+        for (size_t k = 0; k < 4 * (upper.size() / kBoxFloats); ++k) put(upper, k, kEmpty);
+        for (size_t k = 0; k < nup; ++k) {
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            bool inf = false, any = false;
+            for (size_t j = 0; j < 4; ++j) {
+                float t[6];
+                get(lower, 4 * k + j, t);
+                if (!(t[3] > -INFINITY)) continue;
+                any = true;
+                for (int a = 0; a < 3; ++a) {
+                    if (!(t[3 + a] < INFINITY)) inf = true;
+                    lo[a] = std::min(lo[a], (double)t[a] - (double)t[3 + a]);
+                    hi[a] = std::max(hi[a], (double)t[a] + (double)t[3 + a]);
+                }
+            }
+            if (!any) continue;
+            float b[6];
+            box_of(lo, hi, inf, b);
+            put(upper, k, b);
+        }
+    };
+    const size_t nsup = nc / 4, nsg = (nsup + 3) / 4;
+    std::vector<float> wsu, wme;
+    unite(wcl, nsup, wsu);
+    unite(wsu, nsg, wme);
+    // group-local frames: group g of `world` (4 boxes) -> LBoxGroup g
+    auto localise = [&](const std::vector<float>& world, size_t ng, std::vector<float>& out) {
+        out.assign((size_t)kLBoxFloats * (ng + 1), 0.0f);
+        for (size_t g = 0; g < ng + 1; ++g) {
+            float* o = &out[kLBoxFloats * g];
+            double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            bool any = false, inf = false;
+            float bx[4][6];
+            for (size_t j = 0; j < 4; ++j) {
+                if (g < ng) get(world, 4 * g + j, bx[j]);
+                else for (int f = 0; f < 6; ++f) bx[j][f] = kEmpty[f];
+                if (!(bx[j][3] > -INFINITY)) continue;
+                any = true;
+                for (int a = 0; a < 3; ++a) {
+                    if (!(bx[j][3 + a] < INFINITY)) { inf = true; continue; }
+                    lo[a] = std::min(lo[a], (double)bx[j][a] - (double)bx[j][3 + a]);
+                    hi[a] = std::max(hi[a], (double)bx[j][a] + (double)bx[j][3 + a]);
+                }
+            }
+            float Sg[3] = {0.0f, 0.0f, 0.0f};
+            if (any && !inf)
+                for (int a = 0; a < 3; ++a) Sg[a] = (float)(0.5 * (lo[a] + hi[a]));
+            double rg = 0.0;
+            for (size_t j = 0; j < 4; ++j) {
+                float b[6];
+                for (int f = 0; f < 6; ++f) b[f] = bx[j][f];
+                if (b[3] > -INFINITY) {
+                    for (int a = 0; a < 3; ++a) {
+                        const float cl = (float)((double)b[a] - (double)Sg[a]);   // RN_f(C - S)
+                        b[3 + a] = b[3 + a] < INFINITY ? up32((double)b[3 + a] + 0x1.0p-22 * std::fabs((double)cl)) : INFINITY;
+                        b[a] = b[3 + a] < INFINITY ? cl : 0.0f;
+                    }
+                    rg = std::max(rg, std::fabs((double)b[0]) + std::fabs((double)b[1]) + std::fabs((double)b[2]) +
+                                          (double)b[3] + (double)b[4] + (double)b[5]);
+                }
+                for (int f = 0; f < 6; ++f) o[12 * (j / 2) + 2 * f + (j % 2)] = b[f];
+            }
+            o[24] = Sg[0]; o[25] = Sg[1]; o[26] = Sg[2];
+            o[27] = std::isfinite(rg) ? up32(rg) : INFINITY;
+        }
+    };
+    localise(wcl, (nc + 3) / 4, lclb);
+    localise(wsu, nsg, lsup);
+    localise(wme, (nsg + 3) / 4, lmeg);
 }
 
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
@@ -2546,9 +2765,16 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if (c->n_mg) {
             if ((rc = up(&c->meg64, m64.data(), m64.size() * sizeof(float))) != RT_OK) return rc;
             if ((rc = up(&c->meg32, m32.data(), m32.size() * sizeof(float))) != RT_OK) return rc;
-            std::vector<float> lf64, lf32, lr64, lr32;
-            pack_local(c64, L, t64, lf64, lr64);
-            pack_local(c32, L, t32, lf32, lr32);
+            std::vector<float> lf64, lf32, lr64, lr32, q64, q32;
+            pack_local(c64, L, t64, lf64, lr64, q64);
+            pack_local(c32, L, t32, lf32, lr32, q32);
+            std::vector<float> b64[3], b32[3];
+            pack_local_boxes(c64, L, q64, b64[0], b64[1], b64[2], c->l_r2max64, c->l_r2min64);
+            pack_local_boxes(c32, L, q32, b32[0], b32[1], b32[2], c->l_r2max32, c->l_r2min32);
+            for (int lv = 0; lv < 3; ++lv) {
+                if ((rc = up(&c->lbx64[lv], b64[lv].data(), b64[lv].size() * sizeof(float))) != RT_OK) return rc;
+                if ((rc = up(&c->lbx32[lv], b32[lv].data(), b32[lv].size() * sizeof(float))) != RT_OK) return rc;
+            }
             if ((rc = up(&c->lfs64, lf64.data(), lf64.size() * sizeof(float))) != RT_OK) return rc;
             if ((rc = up(&c->lfs32, lf32.data(), lf32.size() * sizeof(float))) != RT_OK) return rc;
             if ((rc = up(&c->lcl64, lr64.data(), lr64.size() * sizeof(float))) != RT_OK) return rc;
@@ -2681,6 +2907,20 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_mg = c->n_mg;
     p.lfsph = (const float*)(f64 ? c->lfs64 : c->lfs32);
     p.lclu = (const float*)(f64 ? c->lcl64 : c->lcl32);
+    p.lclb = (const float*)(f64 ? c->lbx64[0] : c->lbx32[0]);
+    p.lsup = (const float*)(f64 ? c->lbx64[1] : c->lbx32[1]);
+    p.lmeg = (const float*)(f64 ? c->lbx64[2] : c->lbx32[2]);
+    {
+        auto up32 = [](double v) -> float {
+            float f = (float)v;
+            if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
+            return f;
+        };
+        const double r2m = (double)(f64 ? c->l_r2min64 : c->l_r2min32);
+        p.l_r2max = f64 ? c->l_r2max64 : c->l_r2max32;
+        p.l_hir2 = up32(0.5 / r2m);
+        p.l_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m));
+    }
     p.ridx = c->ridx;
     p.n_top = c->n_top;
     p.n_xg = c->n_xg;

@@ -8,7 +8,11 @@
 // evaluation with a quarter of the widening (kappa / 4) must pass too (>= 4x headroom).
 // Cases: clusters of 1..16 spheres with radii spanning 4 decades, rays aimed near tangency to a
 // member from outside, inside and behind the box, axis-parallel rays, scales 0.1..1000.
-// Usage: box_cull_fuzz N F64(0|1) [SEED]
+// LOCAL = 1: the MEGA kernels' local frames (pack_local): the case is moved up to 1000x its size from
+// the origin, r2f is floored per cluster only (2^-10 of its largest), the box is re-centred on a group
+// frame S (C' = RN_f(C - S), H widened by 2^-22 |C'|), the lane uses o' = o - S and the margin from
+// pm = |o'|_1 + |C'|_1 + |H'|_1.
+// Usage: box_cull_fuzz N F64(0|1) [SEED] [LOCAL]
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -74,11 +78,13 @@ int main(int argc, char** argv) {
     const long n = atol(argv[1]);
     const int f64 = atoi(argv[2]);
     if (argc > 3) s = strtoull(argv[3], 0, 0) | 1;
+    const int local = argc > 4 ? atoi(argv[4]) : 0;
     const float u = 0x1.0p-24f;
     long hits = 0, miss = 0, miss_q = 0, miss_0 = 0, culled = 0;
     for (long it = 0; it < n; ++it) {
         const double S = pow(10.0, -1 + 4 * U());
-        const double P[3] = {N() * S, N() * S, N() * S};   // cluster position
+        double P[3] = {N() * S, N() * S, N() * S};   // cluster position
+        if (local) { const double tm = S * pow(10.0, 3 * U()); for (int a = 0; a < 3; ++a) P[a] += N() * tm; }
         const int k = 1 + (int)(U() * 16);
         double cd[16][3], rd[16];
         float cf[16][3], r2f[16];
@@ -94,7 +100,7 @@ int main(int argc, char** argv) {
             rm = fmax(rm, f64 ? rd[j] * rd[j] : (double)((float)rd[j] * (float)rd[j]));
         }
         // pack_filter: floored r2f; pack_sweep: the box; margins (cmax includes |C|_1 + |h|_1)
-        const double floor2 = fmax(rm * 0x1.0p-10, cm * cm * 0x1.0p-16);
+        const double floor2 = local ? rm * 0x1.0p-10 : fmax(rm * 0x1.0p-10, cm * cm * 0x1.0p-16);
         double r2max = 0.0, r2min = INFINITY;
         for (int j = 0; j < k; ++j) {
             const double r2 = f64 ? rd[j] * rd[j] : (double)((float)rd[j] * (float)rd[j]);
@@ -116,7 +122,22 @@ int main(int argc, char** argv) {
             H[a] = up32(hh * (1.0 + 0x1.0p-20) + 0x1.0p-22 * fabs((double)C[a]));
             cb += fabs((double)C[a]) + (double)H[a];
         }
-        const float cmax = up32(fmax(cm, cb)), fr2max = up32(r2max), fr2min = (float)r2min;
+        float cmax = up32(fmax(cm, cb));
+        const float fr2max = up32(r2max), fr2min = (float)r2min;
+        float Sg[3] = {0, 0, 0};
+        if (local) {   // a group frame near the box; the box in it
+            double hs = 0.0;
+            for (int a = 0; a < 3; ++a) hs = fmax(hs, (double)H[a]);
+            double cl = 0.0;
+            for (int a = 0; a < 3; ++a) {
+                Sg[a] = (float)((double)C[a] + N() * hs * 2.0 * U());
+                const float Cl = (float)((double)C[a] - (double)Sg[a]);
+                H[a] = up32((double)H[a] + 0x1.0p-22 * fabs((double)Cl));
+                C[a] = Cl;
+                cl += fabs((double)C[a]) + (double)H[a];
+            }
+            cmax = up32(cl);
+        }
         // a ray near tangency to member j (from outside, inside or behind)
         const int j = (int)(U() * k);
         double D[3] = {N(), N(), N()};
@@ -160,7 +181,9 @@ int main(int argc, char** argv) {
             }
         }
         // nearest_hit's per-lane constants (fp32)
-        const float fd[3] = {(float)D[0], (float)D[1], (float)D[2]}, fo[3] = {(float)O[0], (float)O[1], (float)O[2]};
+        const float fd[3] = {(float)D[0], (float)D[1], (float)D[2]};
+        float fo[3] = {(float)O[0], (float)O[1], (float)O[2]};
+        if (local) for (int a = 0; a < 3; ++a) fo[a] = f64 ? (float)(O[a] - (double)Sg[a]) : fo[a] - Sg[a];   // o' = o - S
         const float on = fabsf(fo[0]) + fabsf(fo[1]) + fabsf(fo[2]);
         const float pm = cmax + on;
         const float mm = 48.0f * 0x1.0p-24f * fmaf(pm, pm, fr2max);
