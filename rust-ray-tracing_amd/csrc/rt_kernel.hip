@@ -149,8 +149,9 @@ template <typename T> struct KParams {
 
 constexpr int kSegShards = 256;
 constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: defocus vectors are +-0
-constexpr int kWavesF32 = 5;   // default min-waves-per-SIMD targets (measured sweep);
+constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep);
 constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
+constexpr int kWavesMegaF32 = 6;   // the mega-level kernels (config E; RT_WAVES=5 selects the W5 build)
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
@@ -1766,6 +1767,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ uint32_t q_sid[QW][QN], q_pix[QW][QN];   // sid | slot << 29, pixel
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
+    // fp32 at 6 waves per SIMD (80 VGPRs): each lane's ray origin and direction are parked in LDS
+    // across the sphere sweeps and the camera batches and re-read right before the scatter, instead
+    // of being held in VGPRs (the allocator otherwise spills them to scratch memory around the sweep).
+#ifdef RT_EXP_NO_PARK
+    constexpr bool kPark = false;
+#else
+    constexpr bool kPark = sizeof(T) == 4 && W >= 6;
+#endif
+    __shared__ T s_park[kPark ? 4 : 1][6][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
@@ -1784,6 +1794,16 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     int hit_i = -1;
     T hit_t = T(0);
     uint32_t slot_item = 0, slot_left = 0;   // lane s < kSlots: pixel item and unfinished samples of slot s
+    auto park = [&](const V3<T>& po, const V3<T>& pd) {
+        T* r = &s_park[kPark ? wave : 0][0][lane];
+        r[0] = po.x; r[64] = po.y; r[128] = po.z; r[192] = pd.x; r[256] = pd.y; r[320] = pd.z;
+    };
+    auto unpark = [&](V3<T>& po, V3<T>& pd) {
+        asm volatile("" ::: "memory");   // re-read: the registers must not be kept across the sweep
+        const T* r = &s_park[kPark ? wave : 0][0][lane];
+        po = mk(r[0], r[64], r[128]);
+        pd = mk(r[192], r[256], r[320]);
+    };
 
     // Hand the lanes of `want` new samples in rank order, opening pixel slots as needed; returns
     // true in the lanes that got one.
@@ -2010,9 +2030,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 pix = q_pix[wave][e];
                 hit_i = q_hit[wave][e];
                 hit_t = q_t[wave][e];
-                d = mk(q_d[wave][0][e], q_d[wave][1][e], q_d[wave][2][e]);
                 const auto& q = *cold_args<T>();
-                o = mk(q.center[0], q.center[1], q.center[2]);
+                const V3<T> pd = mk(q_d[wave][0][e], q_d[wave][1][e], q_d[wave][2][e]);
+                const V3<T> po = mk(q.center[0], q.center[1], q.center[2]);
+                if constexpr (kPark) park(po, pd);
+                else { d = pd; o = po; }
                 c = mk(T(1.0), T(1.0), T(1.0));
                 k = 0;
                 live = true;
@@ -2034,7 +2056,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             asm volatile("" ::"v"(o2.x), "v"(o2.y), "v"(o2.z), "v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(c2.x), "v"(c2.y), "v"(c2.z));
         }
 #endif
+        if constexpr (kPark) unpark(o, d);
         if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
+        if constexpr (kPark) park(o, d);
         if (fresh) {
             k = 0;
             live = true;
@@ -2067,6 +2091,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         // whatever its colour (ray_tracing.rs:495-497), and the scatter draws nothing observable.
         const bool term = live && (!act || skyhit || k + 1 == depth);
         scat = act && hit_i >= 0 && k + 1 < depth;
+        if constexpr (kPark) {
+            if (MODE != kModeV2) { V3<T> po, pd; unpark(po, pd); d = pd; }   // the own-value modes read d
+        }
         terminate(term, skyhit, skyhit ? k : depth, slot, sid, c, d);
         live = live && !term;
     }
@@ -2870,20 +2897,31 @@ static bool check_range(const rt_camera* cam, const rt_tile_range* r) {
 
 static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
 
-// The kernel instantiation for (flags, waves-per-SIMD target, camera batches, mega level).  The mega
-// level (scenes with more than 8 super groups) has its own live-path kernels at the default W; other
-// kernels sweep such scenes from the super boxes (the same result, more box tests).
+// The kernel instantiation for (flags, waves-per-SIMD target, camera batches, mega level).  W < 0:
+// the defaults (RT_WAVES unset).  The mega level (scenes with more than 8 super groups) has its own
+// live-path kernels (fp32 at 5 or 6 waves, default 6; fp64 at 4); at other W such scenes are swept
+// from the super boxes (the same result, more box tests).
 template <typename T, bool CAMQ>
 static void (*pick_kernel(uint32_t flags, int W, bool mega))(KParams<T>) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
-    constexpr int WM = kWavesModes<T>, WD = sizeof(T) == 4 ? kWavesF32 : kWavesF64;
+    constexpr bool F32 = sizeof(T) == 4;
+    constexpr int WM = kWavesModes<T>;
     if (flags & RT_FLAG_MODE_SCALAR) return trace_paths<T, WM, false, kModeScalar, CAMQ>;
     if (flags & RT_FLAG_MODE_VECTORIZED3)
         return r2 ? trace_paths<T, WM, true, kModeV3, CAMQ> : trace_paths<T, WM, false, kModeV3, CAMQ>;
     if (flags & RT_FLAG_MODE_VECTORIZED)
         return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
     if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
-    if (mega && W == WD) return trace_paths<T, WD, false, kModeV2, CAMQ, true>;
+    if (mega) {
+        const int Wm = W < 0 ? (F32 ? kWavesMegaF32 : kWavesF64) : W;
+        if constexpr (F32) {
+            if (Wm == 5) return trace_paths<T, 5, false, kModeV2, CAMQ, true>;
+            if (Wm == 6) return trace_paths<T, 6, false, kModeV2, CAMQ, true>;
+        } else {
+            if (Wm == 4) return trace_paths<T, 4, false, kModeV2, CAMQ, true>;
+        }
+    }
+    if (W < 0) W = F32 ? kWavesF32 : kWavesF64;
     return W >= 6 ? trace_paths<T, 6, false, kModeV2, CAMQ> : W >= 5 ? trace_paths<T, 5, false, kModeV2, CAMQ>
                                                            : trace_paths<T, 4, false, kModeV2, CAMQ>;
 }
@@ -2983,7 +3021,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // launch, so one process can compare them) overrides it for the live-path kernels (pinhole and
     // defocus cameras); the ROOT2 and semantics-mode kernels always run at kWavesModes.
     const char* waves_env = getenv("RT_WAVES");
-    const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : sizeof(T) == 8 ? kWavesF64 : kWavesF32;
+    const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : -1;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
     void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0) : pick_kernel<T, false>(flags, W, p.n_mg > 0);

@@ -189,6 +189,22 @@ def test_config_e_filter_off_same_image(renderer, monkeypatch, flags):
     assert st_off.box_groups > st_on.box_groups and st_off.filter_groups > st_on.filter_groups
 
 
+def test_config_e_wave_builds(renderer, monkeypatch):
+    """The mega-level kernels at 5 (the fp32 default) and 6 waves, and the W4 kernel that sweeps the
+    same scene from the super boxes: one image, one segment count, the oracle's."""
+    flat = rt.scenes.config_scene("E").flatten()
+    cam = cam_for(32, 18)
+    _, lin_o, segs_o, _ = oracle_render(flat, cam, 50, 16, SEED, 0, precision="f32")
+    for wv in (None, "5", "6", "4"):
+        if wv is None:
+            monkeypatch.delenv("RT_WAVES", raising=False)
+        else:
+            monkeypatch.setenv("RT_WAVES", wv)
+        _, lin, st = render(renderer, flat, cam, 50, 16, abi.RT_FLAG_F32)
+        np.testing.assert_array_equal(lin, lin_o, err_msg=f"RT_WAVES={wv}")
+        assert st.ray_segments == segs_o
+
+
 # ---------------------------------------------------------------- vectorized3 (render_vectorized3)
 @pytest.mark.parametrize("spp,prec", [(512, 0), (100, abi.RT_FLAG_F32), (1024, abi.RT_FLAG_F32), (130, 0)])
 def test_vectorized3_large_spp(renderer, spp, prec):
