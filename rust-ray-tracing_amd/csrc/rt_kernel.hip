@@ -1764,7 +1764,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ __attribute__((aligned(16))) T s_stage[4][3][64];   // finish_pixel: 64 positions' values per wave
     __shared__ IssueState s_is[4];
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
-    __shared__ uint32_t q_sid[QW][QN], q_pix[QW][QN];   // sid | slot << 29, pixel
+    __shared__ uint32_t q_sid[QW][QN];   // sid | slot << 29 (the pixel: s_slotpix[slot])
+    __shared__ uint32_t s_slotpix[4][kSlots];   // the pixel of each open slot
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
     // fp32 at 6 waves per SIMD (80 VGPRs): each lane's ray origin and direction are parked in LDS
@@ -1775,7 +1776,13 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
 #else
     constexpr bool kPark = sizeof(T) == 4 && W >= 6;
 #endif
-    __shared__ T s_park[kPark ? 4 : 1][6][64];
+    // the mega-level kernels park the path colour as well (their four-level sweep holds more state)
+#ifdef RT_EXP_PARKC_ALL
+    constexpr bool kParkC = kPark;
+#else
+    constexpr bool kParkC = kPark && MEGA;
+#endif
+    __shared__ T s_park[kPark ? 4 : 1][kParkC ? 9 : 6][64];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
@@ -1803,6 +1810,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const T* r = &s_park[kPark ? wave : 0][0][lane];
         po = mk(r[0], r[64], r[128]);
         pd = mk(r[192], r[256], r[320]);
+    };
+    auto park_c = [&](const V3<T>& pc) {
+        T* r = &s_park[kPark ? wave : 0][kParkC ? 6 : 0][lane];
+        r[0] = pc.x; r[64] = pc.y; r[128] = pc.z;
+    };
+    auto unpark_c = [&]() -> V3<T> {
+        asm volatile("" ::: "memory");
+        const T* r = &s_park[kPark ? wave : 0][kParkC ? 6 : 0][lane];
+        return mk(r[0], r[64], r[128]);
     };
 
     // Hand the lanes of `want` new samples in rank order, opening pixel slots as needed; returns
@@ -1863,6 +1879,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 cur_col = q.col_begin + ci;
                 cur_pix = cur_row * q.W + cur_col;
                 if (lane == s) { slot_item = item; slot_left = spp; }
+                if (lane == 0) s_slotpix[wave][s] = cur_pix;
                 busy |= 1u << s;
                 cur = s;
                 cur_next = 0;
@@ -1996,7 +2013,6 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (push) {
             const uint32_t e = (qhead + qcount + (uint32_t)__popcll(pm & lt_mask)) % kQCap;
             q_sid[wave][e] = bsid | (bslot << 29);
-            q_pix[wave][e] = bpix;
             q_hit[wave][e] = bi;
             q_t[wave][e] = bt;
             q_d[wave][0][e] = bd.x; q_d[wave][1][e] = bd.y; q_d[wave][2][e] = bd.z;
@@ -2027,7 +2043,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 const uint32_t w0 = q_sid[wave][e];
                 sid = w0 & 0x1FFFFFFFu;
                 slot = w0 >> 29;
-                pix = q_pix[wave][e];
+                pix = s_slotpix[wave][slot];
                 hit_i = q_hit[wave][e];
                 hit_t = q_t[wave][e];
                 const auto& q = *cold_args<T>();
@@ -2035,7 +2051,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 const V3<T> po = mk(q.center[0], q.center[1], q.center[2]);
                 if constexpr (kPark) park(po, pd);
                 else { d = pd; o = po; }
-                c = mk(T(1.0), T(1.0), T(1.0));
+                if constexpr (kParkC) park_c(mk(T(1.0), T(1.0), T(1.0)));
+                else c = mk(T(1.0), T(1.0), T(1.0));
                 k = 0;
                 live = true;
                 scat = true;
@@ -2057,8 +2074,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         }
 #endif
         if constexpr (kPark) unpark(o, d);
+        if constexpr (kParkC) c = unpark_c();
         if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
         if constexpr (kPark) park(o, d);
+        if constexpr (kParkC) park_c(c);
         if (fresh) {
             k = 0;
             live = true;
@@ -2094,6 +2113,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if constexpr (kPark) {
             if (MODE != kModeV2) { V3<T> po, pd; unpark(po, pd); d = pd; }   // the own-value modes read d
         }
+        if constexpr (kParkC) c = unpark_c();
         terminate(term, skyhit, skyhit ? k : depth, slot, sid, c, d);
         live = live && !term;
     }
