@@ -142,7 +142,7 @@ template <typename T> struct KParams {
     const float* lclb;         // ... the box levels in group-local frames (pack_local_boxes): per super its
     const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
     const float* lmeg;
-    float l_r2max, l_hir2, l_isr;   // their margin constants: max local r2f, 0.5 / min, 8 u / sqrt(min)
+    float l_r2max, l_hir2, l_isr;   // their margin constants: max local r2f, 48 u 0.5 / min, 8 u / sqrt(min)
     const uint32_t* ridx;
     uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
@@ -674,20 +674,29 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         const f2 B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, 0.0f};
         // MEGA: a box group in its own frame S (pack_local_boxes): o' = o - S (fp64 rays: in double,
         // then rounded), the margin from pm = |o'|_1 + Rg, A = -o'.i, J = |i| (1 + kappa).
+        // Packed where two axes take the same op: o'xy, A'xy = -(o'xy ixy), J'xy = |ixy| kp.  kp =
+        // 1 + m / (2 r2min) + 8 u pm / sqrt(r2min) as fma(pm^2 + r2max, 48 u 0.5 / r2min, fma(pm, 8 u /
+        // sqrt(r2min), 1)): the margin factor folded into the host constant (box_cull_fuzz models this).
+        const f2 nixy = {-ix, -iy}, aixy = {fabsf(ix), fabsf(iy)};
+        const float aiz = fabsf(iz);
         auto lmask = [&](const LBoxGroup& g) -> uint32_t {
             const auto& ql = *cold_args<T>();
-            const float Sx = g.v[24], Sy = g.v[25], Sz = g.v[26], Rg = g.v[27];
-            float opx, opy, opz;
+            const f2 Sxy = {g.v[24], g.v[25]};
+            const float Sz = g.v[26], Rg = g.v[27];
+            f2 opxy;
+            float opz;
             if constexpr (sizeof(T) == 4) {
-                opx = o.x - Sx; opy = o.y - Sy; opz = o.z - Sz;
+                opxy = f2{o.x, o.y} - Sxy;
+                opz = o.z - Sz;
             } else {
-                opx = (float)(o.x - (double)Sx); opy = (float)(o.y - (double)Sy); opz = (float)(o.z - (double)Sz);
+                opxy = f2{(float)(o.x - (double)Sxy.x), (float)(o.y - (double)Sxy.y)};
+                opz = (float)(o.z - (double)Sz);
             }
-            const float pmg = ((fabsf(opx) + fabsf(opy)) + fabsf(opz)) + Rg;
-            const float mg = kFilterMargin * __builtin_fmaf(pmg, pmg, ql.l_r2max);
-            const float kp = 1.0f + __builtin_fmaf(mg, ql.l_hir2, pmg * ql.l_isr);
-            const f2 C1 = {iz, -(opz * iz)}, C2 = {-(opx * ix), -(opy * iy)};
-            const f2 C3 = {fabsf(ix) * kp, fabsf(iy) * kp}, C4 = {fabsf(iz) * kp, 0.0f};
+            const float pmg = ((fabsf(opxy.x) + fabsf(opxy.y)) + fabsf(opz)) + Rg;
+            const float kp = __builtin_fmaf(__builtin_fmaf(pmg, pmg, ql.l_r2max), ql.l_hir2,
+                                            __builtin_fmaf(pmg, ql.l_isr, 1.0f));
+            const f2 C1 = {iz, -(opz * iz)}, C2 = opxy * nixy;
+            const f2 C3 = aixy * f2{kp, kp}, C4 = {aiz * kp, 0.0f};
             return box_mask(g, B0, C1, C2, C3, C4);
         };
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
@@ -796,14 +805,19 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     // basis scaled by it, and o' projected on the scaled basis.
                     const auto& ql = *cold_args<T>();
                     cptr<float> lr = (cptr<float>)__builtin_assume_aligned(ql.lclu, 32);
-                    const float Ckx = lr[8u * kc], Cky = lr[8u * kc + 1u], Ckz = lr[8u * kc + 2u];
+                    const f2 Ckxy = {lr[8u * kc], lr[8u * kc + 1u]};
+                    const float Ckz = lr[8u * kc + 2u];
                     const float Rc = lr[8u * kc + 3u], r2x = lr[8u * kc + 4u], ir2 = lr[8u * kc + 5u];
-                    float opx, opy, opz;
+                    f2 opxy;
+                    float opz;
                     if constexpr (sizeof(T) == 4) {
-                        opx = o.x - Ckx; opy = o.y - Cky; opz = o.z - Ckz;
+                        opxy = f2{o.x, o.y} - Ckxy;
+                        opz = o.z - Ckz;
                     } else {
-                        opx = (float)(o.x - (double)Ckx); opy = (float)(o.y - (double)Cky); opz = (float)(o.z - (double)Ckz);
+                        opxy = f2{(float)(o.x - (double)Ckxy.x), (float)(o.y - (double)Ckxy.y)};
+                        opz = (float)(o.z - (double)Ckz);
                     }
+                    const float opx = opxy.x, opy = opxy.y;
                     const float pmk = ((fabsf(opx) + fabsf(opy)) + fabsf(opz)) + Rc;
                     const float mk = kFilterMargin * __builtin_fmaf(pmk, pmk, r2x);
                     const float sgk = __builtin_amdgcn_rsqf(__builtin_fmaf(mk, ir2, 1.0f));
@@ -2976,7 +2990,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         };
         const double r2m = (double)(f64 ? c->l_r2min64 : c->l_r2min32);
         p.l_r2max = f64 ? c->l_r2max64 : c->l_r2max32;
-        p.l_hir2 = up32(0.5 / r2m);
+        p.l_hir2 = up32((double)kFilterMargin * 0.5 / r2m);
         p.l_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m));
     }
     p.ridx = c->ridx;

@@ -186,8 +186,10 @@ int main(int argc, char** argv) {
         if (local) for (int a = 0; a < 3; ++a) fo[a] = f64 ? (float)(O[a] - (double)Sg[a]) : fo[a] - Sg[a];   // o' = o - S
         const float on = fabsf(fo[0]) + fabsf(fo[1]) + fabsf(fo[2]);
         const float pm = cmax + on;
-        const float mm = 48.0f * 0x1.0p-24f * fmaf(pm, pm, fr2max);
-        const float kap = 1.0f + fmaf(mm, up32(0.5 / fr2min), pm * up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min)));
+        const float isr = up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min));
+        // the sweep's constant (nearest_hit) and the mega kernels' local form (lmask)
+        const float kap = local ? fmaf(fmaf(pm, pm, fr2max), up32(48.0 * 0x1.0p-24 * 0.5 / fr2min), fmaf(pm, isr, 1.0f))
+                                : 1.0f + fmaf(48.0f * 0x1.0p-24f * fmaf(pm, pm, fr2max), up32(0.5 / fr2min), pm * isr);
         const float kq = 1.0f + (kap - 1.0f) * 0.25f;
         float I[3], A[3], J[3], Jq[3], J0[3];
         for (int a = 0; a < 3; ++a) {

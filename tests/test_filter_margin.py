@@ -127,7 +127,14 @@ def test_box_margin_constants_match_kernel():
     fz = open(os.path.join(HERE, "box_cull_fuzz.c")).read()
     assert "1.0f + __builtin_fmaf(m, qa.f_hir2, pm * qa.f_isr)" in src
     assert "p.f_hir2 = up32(0.5 / r2m)" in src and "p.f_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m))" in src
-    assert "1.0f + fmaf(mm, up32(0.5 / fr2min), pm * up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min)))" in fz
+    assert "1.0f + fmaf(48.0f * 0x1.0p-24f * fmaf(pm, pm, fr2max), up32(0.5 / fr2min), pm * isr)" in fz
+    assert "isr = up32(8.0 * 0x1.0p-24 / sqrt((double)fr2min))" in fz
+    # the mega kernels' group-local form (lmask): margin factor folded into l_hir2
+    assert ("__builtin_fmaf(__builtin_fmaf(pmg, pmg, ql.l_r2max), ql.l_hir2,\n"
+            "                                            __builtin_fmaf(pmg, ql.l_isr, 1.0f))") in src
+    assert "p.l_hir2 = up32((double)kFilterMargin * 0.5 / r2m);" in src
+    assert "p.l_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m));" in src
+    assert "fmaf(fmaf(pm, pm, fr2max), up32(48.0 * 0x1.0p-24 * 0.5 / fr2min), fmaf(pm, isr, 1.0f))" in fz
     box = "h * (1.0 + 0x1.0p-20) + 0x1.0p-22 * std::fabs((double)b[a])"
     assert box in src and "hh * (1.0 + 0x1.0p-20) + 0x1.0p-22 * fabs((double)C[a])" in fz
     assert "__builtin_amdgcn_rcpf(fabsf(v) >= 1e-20f ? v : copysignf(1e-20f, v))" in src
