@@ -152,6 +152,9 @@ constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: def
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep);
 constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
 constexpr int kWavesMegaF32 = 6;   // the mega-level kernels (config E; RT_WAVES=5 selects the W5 build)
+// fp32 live-path launches of at least this many samples run at 7 waves per SIMD (72 VGPRs; spills
+// once per sweep, and the LDS of 7 workgroups just fits): +2 % on C and D, a loss on small frames
+constexpr uint64_t kW7Samples = 1ull << 28;
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
@@ -2936,7 +2939,7 @@ static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
 // live-path kernels (fp32 at 5 or 6 waves, default 6; fp64 at 4); at other W such scenes are swept
 // from the super boxes (the same result, more box tests).
 template <typename T, bool CAMQ>
-static void (*pick_kernel(uint32_t flags, int W, bool mega))(KParams<T>) {
+static void (*pick_kernel(uint32_t flags, int W, bool mega, uint64_t samples))(KParams<T>) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
     constexpr bool F32 = sizeof(T) == 4;
     constexpr int WM = kWavesModes<T>;
@@ -2955,7 +2958,10 @@ static void (*pick_kernel(uint32_t flags, int W, bool mega))(KParams<T>) {
             if (Wm == 4) return trace_paths<T, 4, false, kModeV2, CAMQ, true>;
         }
     }
-    if (W < 0) W = F32 ? kWavesF32 : kWavesF64;
+    if (W < 0) W = F32 ? (samples >= kW7Samples ? 7 : kWavesF32) : kWavesF64;
+    if constexpr (F32) {
+        if (W >= 7) return trace_paths<T, 7, false, kModeV2, CAMQ>;
+    }
     return W >= 6 ? trace_paths<T, 6, false, kModeV2, CAMQ> : W >= 5 ? trace_paths<T, 5, false, kModeV2, CAMQ>
                                                            : trace_paths<T, 4, false, kModeV2, CAMQ>;
 }
@@ -3051,14 +3057,16 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_items = rg.row_count * rg.col_count;
 
     // Persistent grid: as many 4-wave workgroups as stay resident, never more waves than pixels.
-    // Minimum waves per SIMD the register allocation targets.  RT_WAVES (4, 5, 6; read at every
+    // Minimum waves per SIMD the register allocation targets.  RT_WAVES (4..7; read at every
     // launch, so one process can compare them) overrides it for the live-path kernels (pinhole and
     // defocus cameras); the ROOT2 and semantics-mode kernels always run at kWavesModes.
     const char* waves_env = getenv("RT_WAVES");
     const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : -1;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
-    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0) : pick_kernel<T, false>(flags, W, p.n_mg > 0);
+    const uint64_t samples = (uint64_t)p.n_items * spp;
+    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, samples)
+                                    : pick_kernel<T, false>(flags, W, p.n_mg > 0, samples);
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
         p.camf = (const float*)(f64 ? c->camf64 : c->camf32);
