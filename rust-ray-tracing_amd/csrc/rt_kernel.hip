@@ -152,9 +152,9 @@ constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: def
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep);
 constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
 constexpr int kWavesMegaF32 = 6;   // the mega-level kernels (config E; RT_WAVES=5 selects the W5 build)
-// fp32 live-path launches of at least this many samples run at 7 waves per SIMD (72 VGPRs; spills
-// once per sweep, and the LDS of 7 workgroups just fits): +2 % on C and D, a loss on small frames
-constexpr uint64_t kW7Samples = 1ull << 28;
+// RT_WAVES=7 selects a 7-waves-per-SIMD fp32 live-path build (72 VGPRs; the LDS of 7 workgroups
+// just fits): +2 % on C and D, but it spills ~7 VGPRs around every sweep, and the scratch lines
+// (4 MB per XCD) push HBM writes from 23 to 41 B/sample, so the default stays at 6
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
 constexpr int kSegStride = 16;  // u64 per shard (128 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
@@ -2958,7 +2958,8 @@ static void (*pick_kernel(uint32_t flags, int W, bool mega, uint64_t samples))(K
             if (Wm == 4) return trace_paths<T, 4, false, kModeV2, CAMQ, true>;
         }
     }
-    if (W < 0) W = F32 ? (samples >= kW7Samples ? 7 : kWavesF32) : kWavesF64;
+    (void)samples;
+    if (W < 0) W = F32 ? kWavesF32 : kWavesF64;
     if constexpr (F32) {
         if (W >= 7) return trace_paths<T, 7, false, kModeV2, CAMQ>;
     }
