@@ -131,6 +131,7 @@ template <typename T> struct KParams {
     // n_xg leading groups of always-exact spheres, then cluster k at groups n_xg + 4k .. + 3
     const T* rsph;
     const float* rfsph;
+    const uint32_t* xrec;      // fp32: per slot group {r² of pair 0, r² of pair 1, 4 scene indices} (32 B)
     const float* ftop;
     const float* fsup;         // super boxes (4 clusters each), 4 per group
     const float* fmeg;         // mega boxes (4 supers each), 4 per group; n_mg groups, 0: no mega level
@@ -757,6 +758,43 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     if (((pairs >> (j >> 1)) & 1u) && cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
             }
         };
+        // fp32, scene-frame filter groups (not MEGA): the exact test of a taken group takes the centres
+        // from its filter group, already in SGPRs (the same fp32 values, pack_filter / pack_sweep), and
+        // loads only the group's r² and scene indices (one s_load_dwordx8 instead of the 64-byte exact
+        // group plus the index table behind a kernel-argument load)
+        auto exact4f = [&](const SphGroup<float>& cur, uint32_t g, uint32_t pairs) {
+            KSTAT(0);
+            if constexpr (sizeof(T) == 4) {
+                const auto& qx = *cold_args<T>();
+                cptr<uint32_t> xr = (cptr<uint32_t>)__builtin_assume_aligned(qx.xrec, 32);
+                uint32_t rec[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rec[j] = xr[8u * g + (uint32_t)j];
+                const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
+                const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
+                const f2 na = {-a, -a};
+#pragma unroll
+                for (uint32_t q = 0; q < 2; ++q) {
+                    if (!((pairs >> q) & 1u)) continue;
+                    f2 hb, disc;
+                    const float* v = &cur.v[8 * q];
+                    const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]};
+                    const f2 r2 = {__uint_as_float(rec[2 * q]), __uint_as_float(rec[2 * q + 1])};
+                    const f2 ocx = ox - cx, ocy = oy - cy, ocz = oz - cz;             // :252
+                    if constexpr (SCALAR) {                                           // objects.rs:217-222
+                        hb = (ocx * dx + ocy * dy) + ocz * dz;
+                        const f2 c = ((ocx * ocx + ocy * ocy) + ocz * ocz) - r2;
+                        disc = hb * hb - (-na) * c;
+                    } else {
+                        hb = fma2(ocz, dz, fma2(ocy, dy, ocx * dx));                  // :255
+                        const f2 c = fma2(ocz, ocz, fma2(ocy, ocy, ocx * ocx)) - r2;  // :256
+                        disc = fma2(hb, hb, na * c);                                  // :257
+                    }
+                    if (cand_f(hb.x, disc.x)) hit(hb.x, disc.x, rec[4 + 2 * q]);
+                    if (cand_f(hb.y, disc.y)) hit(hb.y, disc.y, rec[5 + 2 * q]);
+                }
+            }
+        };
 #ifdef RT_EXP_FLAT_SWEEP
         auto group = [&](const SphGroup<float>& cur, uint32_t g) {
             uint32_t s0, s1;
@@ -843,7 +881,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                             pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
                                     (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
                         n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
-                        exact4(g0 + g, pairs);
+#ifndef RT_EXP_NO_XREC
+                        if constexpr (sizeof(T) == 4 && !MEGA && !CAMT) exact4f(cur, g0 + g, pairs);
+                        else
+#endif
+                            exact4(g0 + g, pairs);
                     }
                 });
             }
@@ -2181,6 +2223,7 @@ struct rt_context {
     void* cull64 = nullptr; void* cull32 = nullptr; // camera cone-cull records (fp32; rebuilt per launch)
     uint32_t n_cull = 0;                            // records: n_spheres rounded up to 64, + 64 padding
     void* rsph64 = nullptr; void* rsph32 = nullptr; // general sweep: slot-order exact groups
+    void* xrec32 = nullptr;                          // fp32: the exact test's r² and scene indices per group
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
     void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
@@ -2281,6 +2324,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->camx64); (void)hipFree(c->camx32); (void)hipFree(c->cull64); (void)hipFree(c->cull32);
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
+    (void)hipFree(c->xrec32);
+    c->xrec32 = nullptr;
     (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
     (void)hipFree(c->sup64); (void)hipFree(c->sup32);
     c->sup64 = c->sup32 = nullptr;
@@ -2905,6 +2950,17 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->top64, t64.data(), t64.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->top32, t32.data(), t32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up((void**)&c->ridx, ridx.data(), ridx.size() * sizeof(uint32_t))) != RT_OK) return rc;
+        {   // fp32 exact-test records: a walked group's centres are its filter group's (the same fp32
+            // values), so a taken group loads only these 32 bytes (nearest_hit, exact4f)
+            const size_t ng = rg32.size() / 16;
+            std::vector<uint32_t> xr((size_t)8 * ng, 0xFFFFFFFFu);
+            for (size_t g = 0; g < ng; ++g) {
+                for (int q = 0; q < 2; ++q)
+                    for (int h = 0; h < 2; ++h) memcpy(&xr[8 * g + 2 * q + h], &rg32[16 * g + 8 * q + 6 + h], 4);
+                for (int j = 0; j < 4; ++j) if (4 * g + j < ridx.size()) xr[8 * g + 4 + j] = ridx[4 * g + j];
+            }
+            if ((rc = up((void**)&c->xrec32, xr.data(), xr.size() * sizeof(uint32_t))) != RT_OK) return rc;
+        }
         HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
         HIPCHK(hipMalloc(&c->camf32, f32g.size() * sizeof(float)));
     }
@@ -2980,6 +3036,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_fgroups = c->n_fgroups;
     p.rsph = (const T*)(f64 ? c->rsph64 : c->rsph32);
     p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
+    p.xrec = f64 ? nullptr : (const uint32_t*)c->xrec32;
     p.ftop = (const float*)(f64 ? c->top64 : c->top32);
     p.fsup = (const float*)(f64 ? c->sup64 : c->sup32);
     p.fmeg = (const float*)(f64 ? c->meg64 : c->meg32);
