@@ -153,6 +153,10 @@ constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: def
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep);
 constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
 constexpr int kWavesMegaF32 = 6;   // the mega-level kernels (config E; RT_WAVES=5 selects the W5 build)
+// fp32 launches below this many samples per resident W6 wave run at W5: W6's extra waves then split
+// the pixels thinner and the tail costs more than the occupancy gains (tools/waves_ab.py: an 8-way
+// shard of C, 21 600 samples per wave, is 6 % slower at W6; the 4-way shard, 43 200, 5.6 % faster)
+constexpr uint64_t kW6SamplesPerWave = 32768;
 // RT_WAVES=7 selects a 7-waves-per-SIMD fp32 live-path build (72 VGPRs; the LDS of 7 workgroups
 // just fits): +2 % on C and D, but it spills ~7 VGPRs around every sweep, and the scratch lines
 // (4 MB per XCD) push HBM writes from 23 to 41 B/sample, so the default stays at 6
@@ -2995,7 +2999,7 @@ static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
 // live-path kernels (fp32 at 5 or 6 waves, default 6; fp64 at 4); at other W such scenes are swept
 // from the super boxes (the same result, more box tests).
 template <typename T, bool CAMQ>
-static void (*pick_kernel(uint32_t flags, int W, bool mega, uint64_t samples))(KParams<T>) {
+static void (*pick_kernel(uint32_t flags, int W, bool mega, bool big))(KParams<T>) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
     constexpr bool F32 = sizeof(T) == 4;
     constexpr int WM = kWavesModes<T>;
@@ -3006,7 +3010,7 @@ static void (*pick_kernel(uint32_t flags, int W, bool mega, uint64_t samples))(K
         return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
     if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
     if (mega) {
-        const int Wm = W < 0 ? (F32 ? kWavesMegaF32 : kWavesF64) : W;
+        const int Wm = W < 0 ? (F32 ? (big ? kWavesMegaF32 : 5) : kWavesF64) : W;
         if constexpr (F32) {
             if (Wm == 5) return trace_paths<T, 5, false, kModeV2, CAMQ, true>;
             if (Wm == 6) return trace_paths<T, 6, false, kModeV2, CAMQ, true>;
@@ -3014,8 +3018,7 @@ static void (*pick_kernel(uint32_t flags, int W, bool mega, uint64_t samples))(K
             if (Wm == 4) return trace_paths<T, 4, false, kModeV2, CAMQ, true>;
         }
     }
-    (void)samples;
-    if (W < 0) W = F32 ? kWavesF32 : kWavesF64;
+    if (W < 0) W = F32 ? (big ? kWavesF32 : 5) : kWavesF64;
     if constexpr (F32) {
         if (W >= 7) return trace_paths<T, 7, false, kModeV2, CAMQ>;
     }
@@ -3122,9 +3125,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : -1;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
-    const uint64_t samples = (uint64_t)p.n_items * spp;
-    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, samples)
-                                    : pick_kernel<T, false>(flags, W, p.n_mg > 0, samples);
+    const bool big = (uint64_t)p.n_items * spp >= kW6SamplesPerWave * 24u * (uint64_t)c->n_cu;
+    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, big)
+                                    : pick_kernel<T, false>(flags, W, p.n_mg > 0, big);
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
         p.camf = (const float*)(f64 ? c->camf64 : c->camf32);
