@@ -877,13 +877,10 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
                     // rejects them as well (the filter passes every sphere the reference can hit).
                     if (__ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1))) != 0ull) {
-                        // only the sphere pairs some lane passes (one compare each, taken groups only)
-                        uint32_t pairs = 3u;
-#ifndef RT_EXP_PAIRS_F64
-                        if constexpr (sizeof(T) == 4)
-#endif
-                            pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
-                                    (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
+                        // only the sphere pairs some lane passes (one compare each, taken groups
+                        // only; fp64 too since the ray left scratch memory: +1.0 % at C)
+                        const uint32_t pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
+                                               (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
                         n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
 #ifndef RT_EXP_NO_XREC
                         if constexpr (sizeof(T) == 4 && !MEGA && !CAMT) exact4f(cur, g0 + g, pairs);
