@@ -189,6 +189,23 @@ def test_config_e_filter_off_same_image(renderer, monkeypatch, flags):
     assert st_off.box_groups > st_on.box_groups and st_off.filter_groups > st_on.filter_groups
 
 
+def test_launch_size_rule_same_pixels(renderer, monkeypatch):
+    """The default occupancy depends on the launch's size (W6 for the whole frame of C, W5 for an
+    8-way shard, kW6SamplesPerWave): the shard's rows must equal the same rows of the whole frame, bit
+    for bit, with RT_WAVES unset."""
+    monkeypatch.delenv("RT_WAVES", raising=False)
+    w, h, _, spp, depth = rt.scenes.CONFIGS["C"]
+    flat = rt.scenes.config_scene("C").flatten()
+    cam = cam_for(w, h)
+    rgb_f, lin_f, _ = render(renderer, flat, cam, depth, spp, abi.RT_FLAG_F32)
+    for rank in (0, 5):
+        tile = rt.parallel.shard_range(w, h, 8, rank)
+        rgb_s, lin_s, st = render(renderer, flat, cam, depth, spp, abi.RT_FLAG_F32, tile=tile)
+        rows = np.arange(rank, h, 8)
+        np.testing.assert_array_equal(lin_s.reshape(len(rows), w, 3), lin_f.reshape(h, w, 3)[rows])
+        np.testing.assert_array_equal(rgb_s.reshape(len(rows), w, 3), rgb_f.reshape(h, w, 3)[rows])
+
+
 def test_config_e_wave_builds(renderer, monkeypatch):
     """The mega-level kernels at 5 (the fp32 default) and 6 waves, and the W4 kernel that sweeps the
     same scene from the super boxes: one image, one segment count, the oracle's."""
