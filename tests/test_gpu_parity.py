@@ -98,6 +98,13 @@ def test_fp64_2048(renderer, scene_100):
     assert_parity(renderer, scene_100, cam_for(4, 3), 50, 2048, 0)
 
 
+def test_wide_records(renderer, scene_100):
+    """The scratch formats' wide variants (PScratch): more than 65532 positions per pixel take a u32
+    position map, depth > 254 takes u32 termination bounces."""
+    assert_parity(renderer, scene_100, cam_for(2, 1), 50, 70001, abi.RT_FLAG_F32)   # P = 70004 > 65532
+    assert_parity(renderer, scene_100, cam_for(16, 9), 300, 16, 0)                 # depth 300 > 254
+
+
 def test_spp_limit(renderer, scene_100):
     with pytest.raises(rt.RtError) as e:
         gpu(renderer, scene_100, cam_for(2, 2), 50, (1 << 20) + 1, flags=abi.RT_FLAG_F32)
