@@ -379,7 +379,12 @@ __device__ __forceinline__ uint32_t cam_filter_group(const SphGroup<float>& cur,
 // B0 = {ix, iy}, B1 = {iz, Az}, B2 = {Ax, Ay}, B3 = {Jx, Jy}, B4 = {Jz, -}, broadcast with op_sel;
 // 9 packed FMAs per box pair, then max3/min3 per box.  Returns the 4-bit wave mask of clusters
 // that pass for some lane.
-__device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
+// bt (>= the lane's best hit t so far, +inf before any hit) also culls a box the ray enters only past
+// its best hit: tn > bt.  The widened box holds every point o + t* d of a root t* the reference could
+// report for a member, and the computed near time is <= t* (the margin covers its rounding;
+// tests/box_cull_fuzz.c checks tn <= t* directly), so such a box holds no hit with t* <= bt: none that
+// could replace the best (ties need t* == best).  The test is tn0 = max(tn, 0) <= min(tf, bt).
+__device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4, float bt) {
     f2 ux, uy, uz, nx, ny, nz;
     const f2 cx = {v[0], v[1]}, cy = {v[2], v[3]}, cz = {v[4], v[5]}, hx = {v[6], v[7]}, hy = {v[8], v[9]},
              hz = {v[10], v[11]};
@@ -402,7 +407,7 @@ __device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2
     // (two v_max_f32 x, x per box; these values come from FMAs, never signalling NaNs), and the
     // ballot's bool took a round trip through a VGPR.  v_cmp_e64 writes 0 for inactive lanes, as a
     // ballot does.
-    auto pass = [](float nx, float ny, float nz, float fx, float fy, float fz, auto bitc) -> uint32_t {
+    auto pass = [bt](float nx, float ny, float nz, float fx, float fy, float fz, auto bitc) -> uint32_t {
         constexpr uint32_t bit = decltype(bitc)::value;
         float tn, tf;
         unsigned long long m;
@@ -411,11 +416,13 @@ __device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2
             "v_max3_f32 %[tn], %[nx], %[ny], %[nz]\n\t"
             "v_min3_f32 %[tf], %[fx], %[fy], %[fz]\n\t"
             "v_max_f32 %[tn], 0, %[tn]\n\t"
+            "v_min_f32 %[tf], %[tf], %[bt]\n\t"
             "v_cmp_nlt_f32_e64 %[m], %[tf], %[tn]\n\t"
             "s_cmp_lg_u64 %[m], 0\n\t"
             "s_cselect_b32 %[r], %[bit], 0"
             : [tn] "=&v"(tn), [tf] "=&v"(tf), [m] "=&s"(m), [r] "=s"(r)
-            : [nx] "v"(nx), [ny] "v"(ny), [nz] "v"(nz), [fx] "v"(fx), [fy] "v"(fy), [fz] "v"(fz), [bit] "n"(bit)
+            : [nx] "v"(nx), [ny] "v"(ny), [nz] "v"(nz), [fx] "v"(fx), [fy] "v"(fy), [fz] "v"(fz), [bt] "v"(bt),
+              [bit] "n"(bit)
             : "scc");
         return r;
     };
@@ -423,11 +430,11 @@ __device__ __forceinline__ uint32_t box_pair(const float* v, f2 B0, f2 B1, f2 B2
     return __builtin_amdgcn_readfirstlane(pass(nx.x, ny.x, nz.x, ux.x, uy.x, uz.x, std::integral_constant<uint32_t, 1>{}) |
                                           pass(nx.y, ny.y, nz.y, ux.y, uy.y, uz.y, std::integral_constant<uint32_t, 2>{}));
 }
-__device__ __forceinline__ uint32_t box_mask(const BoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
-    return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
+__device__ __forceinline__ uint32_t box_mask(const BoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4, float bt) {
+    return box_pair(&cur.v[0], B0, B1, B2, B3, B4, bt) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4, bt) << 2);
 }
-__device__ __forceinline__ uint32_t box_mask(const LBoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4) {
-    return box_pair(&cur.v[0], B0, B1, B2, B3, B4) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4) << 2);
+__device__ __forceinline__ uint32_t box_mask(const LBoxGroup& cur, f2 B0, f2 B1, f2 B2, f2 B3, f2 B4, float bt) {
+    return box_pair(&cur.v[0], B0, B1, B2, B3, B4, bt) | (box_pair(&cur.v[12], B0, B1, B2, B3, B4, bt) << 2);
 }
 
 // The object loop of trace_vectorized2 for one enabled ray (ray_tracing.rs:399-403): returns the
@@ -685,6 +692,15 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // Packed where two axes take the same op: o'xy, A'xy = -(o'xy ixy), J'xy = |ixy| kp.  kp =
         // 1 + m / (2 r2min) + 8 u pm / sqrt(r2min) as fma(pm^2 + r2max, 48 u 0.5 / r2min, fma(pm, 8 u /
         // sqrt(r2min), 1)): the margin factor folded into the host constant (box_cull_fuzz models this).
+        // The best hit so far as a box-time bound (box_pair): fp64 rounds it up to a float.
+        auto btf = [&]() -> float {
+#ifdef RT_EXP_NO_PRUNE
+            return INFINITY;
+#else
+            if constexpr (sizeof(T) == 4) return best_t;
+            else return (float)best_t * (1.0f + 0x1.0p-22f);   // RN(RN(b) (1 + 2^-22)) > b (b > 0)
+#endif
+        };
         const f2 nixy = {-ix, -iy}, aixy = {fabsf(ix), fabsf(iy)};
         const float aiz = fabsf(iz);
         auto lmask = [&](const LBoxGroup& g) -> uint32_t {
@@ -705,7 +721,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                                             __builtin_fmaf(pmg, ql.l_isr, 1.0f));
             const f2 C1 = {iz, -(opz * iz)}, C2 = opxy * nixy;
             const f2 C3 = aixy * f2{kp, kp}, C4 = {aiz * kp, 0.0f};
-            return box_mask(g, B0, C1, C2, C3, C4);
+            return box_mask(g, B0, C1, C2, C3, C4, btf());
         };
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
         // the sphere pairs set in `pairs` (bit q: spheres 4g+2q, 4g+2q+1; wave-uniform).
@@ -835,7 +851,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             ++n_box;
             uint32_t mask;
             if constexpr (MEGA) mask = lmask(load_lbox((cptr<float>)__builtin_assume_aligned(qa.lclb, 64), sup));
-            else mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4);
+            else mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4, btf());
             while (mask != 0u) {
                 const uint32_t kc = 4u * sup + (uint32_t)__builtin_ctz(mask);   // cluster
                 const uint32_t g0 = nxg + 4u * kc;
@@ -926,7 +942,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 n_box += min(8u, nsg - t0);
                 box_loop(fs + kBoxFloats * t0, min(8u, nsg - t0), [&](const BoxGroup& cur, uint32_t t) {
                     KSTAT(5);
-                    tmask |= box_mask(cur, B0, B1, B2, B3, B4) << (4u * t);
+                    tmask |= box_mask(cur, B0, B1, B2, B3, B4, btf()) << (4u * t);
                 });
                 while (tmask != 0u) {
                     const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);

@@ -3,7 +3,9 @@
 // Claim checked: whenever the reference's sphere test finds a valid root -- hit_packed under Q1
 // (objects.rs:249-290), hit_packed with root2, or the scalar Sphere::hit (objects.rs:216-247), in
 // fp32 or fp64 -- for a member of a cluster, the kernel's slab test of that ray against the
-// cluster's box passes.  The box and the lane's margin are computed exactly as the host and the
+// cluster's box passes, and passes with the best-hit bound at that root too (box_pair's bt: the
+// computed near time is <= the smallest root any of those tests reports, so a box entered only past
+// the lane's best hit can be skipped).  The box and the lane's margin are computed exactly as the host and the
 // kernel do (fp32 filter records, floored r2f, kappa from m = 48 u (pm^2 + r2max)).  A second
 // evaluation with a quarter of the widening (kappa / 4) must pass too (>= 4x headroom).
 // Cases: clusters of 1..16 spheres with radii spanning 4 decades, rays aimed near tangency to a
@@ -29,7 +31,8 @@ static float rcp(float x) {
     return r;
 }
 
-static int hits_f(const float o[3], const float d[3], const float c[3], float r) {
+static double vmin(double t, double x, double lo) { return (x >= lo && x < INFINITY && x < t) ? x : t; }
+static double hits_f(const float o[3], const float d[3], const float c[3], float r) {
     const float oc[3] = {o[0] - c[0], o[1] - c[1], o[2] - c[2]}, r2 = r * r;
     const float a = fmaf(d[2], d[2], fmaf(d[1], d[1], d[0] * d[0]));
     const float hb = fmaf(oc[2], d[2], fmaf(oc[1], d[1], oc[0] * d[0]));
@@ -37,15 +40,17 @@ static int hits_f(const float o[3], const float d[3], const float c[3], float r)
     const float disc = fmaf(hb, hb, (-a) * cc);
     const float sd = sqrtf(disc), ia = 1.0f / a;
     const float r1 = (-hb - sd) * ia, rr2 = (-hb + sd) * ia;
-    if ((r1 >= 0.001f && r1 < INFINITY) || (rr2 >= 0.001f && rr2 < INFINITY)) return 1;
+    double t = INFINITY;
+    t = vmin(t, r1, 0.001f); t = vmin(t, rr2, 0.001f);
     const float as = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     const float hs = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
     const float cs = (oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2]) - r2;
     const float ds = hs * hs - as * cs, sds = sqrtf(ds);
     const float q1 = (-hs - sds) / as, q2 = (-hs + sds) / as;
-    return (q1 >= 0.001f && q1 < INFINITY) || (q2 >= 0.001f && q2 < INFINITY);
+    t = vmin(t, q1, 0.001f); t = vmin(t, q2, 0.001f);
+    return t;
 }
-static int hits_d(const double o[3], const double d[3], const double c[3], double r) {
+static double hits_d(const double o[3], const double d[3], const double c[3], double r) {
     const double oc[3] = {o[0] - c[0], o[1] - c[1], o[2] - c[2]}, r2 = r * r;
     const double a = fma(d[2], d[2], fma(d[1], d[1], d[0] * d[0]));
     const double hb = fma(oc[2], d[2], fma(oc[1], d[1], oc[0] * d[0]));
@@ -53,13 +58,15 @@ static int hits_d(const double o[3], const double d[3], const double c[3], doubl
     const double disc = fma(hb, hb, (-a) * cc);
     const double sd = sqrt(disc), ia = 1.0 / a;
     const double r1 = (-hb - sd) * ia, rr2 = (-hb + sd) * ia;
-    if ((r1 >= 0.001 && r1 < INFINITY) || (rr2 >= 0.001 && rr2 < INFINITY)) return 1;
+    double t = INFINITY;
+    t = vmin(t, r1, 0.001); t = vmin(t, rr2, 0.001);
     const double as = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
     const double hs = oc[0] * d[0] + oc[1] * d[1] + oc[2] * d[2];
     const double cs = (oc[0] * oc[0] + oc[1] * oc[1] + oc[2] * oc[2]) - r2;
     const double ds = hs * hs - as * cs, sds = sqrt(ds);
     const double q1 = (-hs - sds) / as, q2 = (-hs + sds) / as;
-    return (q1 >= 0.001 && q1 < INFINITY) || (q2 >= 0.001 && q2 < INFINITY);
+    t = vmin(t, q1, 0.001); t = vmin(t, q2, 0.001);
+    return t;
 }
 
 // box_pair's test for one box (kernel arithmetic, fp32)
@@ -72,6 +79,17 @@ static int box_pass(const float C[3], const float h[3], const float i[3], const 
     }
     const float tn = fmaxf(fmaxf(n[0], n[1]), n[2]), tf = fminf(fminf(f[0], f[1]), f[2]);
     return !(tf - tn < 0.0f) && !(tf < 0.0f);
+}
+// the same with the best-hit bound bt (box_pair: max(tn, 0) <= min(tf, bt)), as the kernel orders it
+static int box_pass_bt(const float C[3], const float h[3], const float i[3], const float A[3], const float J[3], float bt) {
+    float n[3], f[3];
+    for (int a = 0; a < 3; ++a) {
+        const float u = fmaf(C[a], i[a], A[a]);
+        n[a] = fmaf(h[a], -J[a], u);
+        f[a] = fmaf(h[a], J[a], u);
+    }
+    const float tn = fmaxf(fmaxf(fmaxf(n[0], n[1]), n[2]), 0.0f), tf = fminf(fminf(fminf(f[0], f[1]), f[2]), bt);
+    return !(tf < tn);
 }
 
 int main(int argc, char** argv) {
@@ -171,15 +189,18 @@ int main(int argc, char** argv) {
             if (!f64) for (int a = 0; a < 3; ++a) { O[a] = (float)O[a]; D[a] = (float)D[a]; }
         }
         if (!f64) for (int a = 0; a < 3; ++a) { O[a] = (float)O[a]; D[a] = (float)D[a]; }
-        int any = 0;
+        double tmin = INFINITY;   // the smallest root any of the reference's tests reports for a member
         for (int m = 0; m < k; ++m) {
-            if (f64) any |= hits_d(O, D, cd[m], rd[m]);
+            if (f64) tmin = fmin(tmin, hits_d(O, D, cd[m], rd[m]));
             else {
                 const float of[3] = {(float)O[0], (float)O[1], (float)O[2]}, df[3] = {(float)D[0], (float)D[1], (float)D[2]};
                 const float cc[3] = {(float)cd[m][0], (float)cd[m][1], (float)cd[m][2]};
-                any |= hits_f(of, df, cc, (float)rd[m]);
+                tmin = fmin(tmin, hits_f(of, df, cc, (float)rd[m]));
             }
         }
+        const int any = tmin < INFINITY;
+        // the best-hit bound at that root: the kernel's bt for a best hit t* (fp64: rounded up)
+        const float bt = f64 ? (float)tmin * (1.0f + 0x1.0p-22f) : (float)tmin;
         // nearest_hit's per-lane constants (fp32)
         const float fd[3] = {(float)D[0], (float)D[1], (float)D[2]};
         float fo[3] = {(float)O[0], (float)O[1], (float)O[2]};
@@ -200,11 +221,12 @@ int main(int argc, char** argv) {
             J0[a] = fabsf(I[a]);
         }
         const int pass = box_pass(C, H, I, A, J), pass_q = box_pass(C, H, I, A, Jq), pass_0 = box_pass(C, H, I, A, J0);
+        const int pass_b = box_pass_bt(C, H, I, A, J, bt), pass_bq = box_pass_bt(C, H, I, A, Jq, bt);
         if (!pass) ++culled;
         if (any) {
             ++hits;
-            if (!pass) ++miss;
-            if (!pass_q) ++miss_q;
+            if (!pass || !pass_b) ++miss;
+            if (!pass_q || !pass_bq) ++miss_q;
             if (!pass_0) ++miss_0;
         }
     }
