@@ -33,6 +33,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <initializer_list>
 #include <chrono>
 #include <cmath>
 #include <limits>
@@ -144,6 +146,11 @@ template <typename T> struct KParams {
     const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
     const float* lmeg;
     float l_r2max, l_hir2, l_isr;   // their margin constants: max local r2f, 48 u 0.5 / min, 8 u / sqrt(min)
+    // ... and the mega walk's order (<= 64 megas): a grid over the megas' union, per cell 4 u64 words
+    // {touching, within 1/4 of a mega's size, within 1/2, 0} (pack_mega_tiers)
+    const uint64_t* mtiers;
+    float mt_lo[3], mt_inv;
+    uint32_t mt_n[3];
     const uint32_t* ridx;
     uint32_t n_top, n_xg, n_xs;   // n_xs: always-exact spheres (the rest of their last group are dummies)
 };
@@ -915,24 +922,78 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             cptr<float> lm = (cptr<float>)__builtin_assume_aligned(qa.lmeg, 64);
             cptr<float> ls = (cptr<float>)__builtin_assume_aligned(qa.lsup, 64);
             const uint32_t ntg = qa.n_mg;
-            for (uint32_t t0 = 0; t0 < ntg; t0 += 8u) {
-                uint32_t tmask = 0;
-                n_box += min(8u, ntg - t0);
-                lbox_loop(lm + 32u * t0, min(8u, ntg - t0), [&](const LBoxGroup& cur, uint32_t t) {
-                    KSTAT(5);
-                    tmask |= lmask(cur) << (4u * t);
-                });
-                while (tmask != 0u) {
-                    const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctz(tmask);
-                    tmask &= tmask - 1u;
-                    if (nd >= nsg) break;   // padding megas (empty boxes; see below)
-                    ++n_box;
-                    uint32_t smask = lmask(load_lbox(ls, nd));
-                    while (smask != 0u) {
-                        const uint32_t sup = 4u * nd + (uint32_t)__builtin_ctz(smask);
-                        smask &= smask - 1u;
-                        if (sup >= ntop) break;
-                        walk_super(sup);
+            // the supers of one passing mega
+            auto walk_mega = [&](uint32_t nd) {
+                ++n_box;
+                uint32_t smask = lmask(load_lbox(ls, nd));
+                if (4u * nd + 4u > ntop) smask &= (1u << (ntop - 4u * nd)) - 1u;   // padding supers
+                while (smask != 0u) {
+                    const uint32_t sup = 4u * nd + (uint32_t)__builtin_ctz(smask);
+                    smask &= smask - 1u;
+                    walk_super(sup);
+                }
+            };
+            // Up to 64 megas (16 groups) at once: test them all, then walk the passing ones in tiers
+            // of distance from the reference point's grid cell (the host's mega tier table: the megas
+            // whose box touches the cell, then those within a quarter and a half of a mega's size,
+            // then the rest), index order inside a tier.  More megas: chunks of 32 in index order.
+            const uint32_t span = ntg <= 16u ? 16u : 8u;
+            for (uint32_t t0 = 0; t0 < ntg; t0 += span) {
+                const uint32_t nt = min(span, ntg - t0);
+                uint64_t tm = 0;
+                n_box += nt;
+                for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
+                    lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
+                        KSTAT(5);
+                        tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
+                    });
+                if (4u * (t0 + nt) > nsg) tm &= (1ull << (nsg - 4u * t0)) - 1ull;   // padding megas (empty boxes)
+#ifndef RT_EXP_TIERS
+#define RT_EXP_TIERS 3
+#endif
+                // RT_EXP_TIERS 3 (default): T0 and T1 held in SGPRs, T2 merged into the rest; 4: all four
+                // tiers, each mask re-read per tier (scalar loads); 2: T0 only.  Same-box E fp32: 9819 /
+                // 9773 / 9794, against 9328 in index order (profiles/r02/experiments/tiers.txt)
+                uint32_t ci = 0xFFFFFFFFu;   // the reference cell's table row (none: one tier)
+#if !defined(RT_EXP_NO_ORDER)
+                if (span == 16u) {
+                    const auto& qt = *cold_args<T>();
+                    auto cell = [](float v, float lo, float inv, uint32_t n) -> uint32_t {
+                        const float c = fminf(fmaxf((v - lo) * inv, 0.0f), (float)(n - 1u));   // NaN -> 0
+                        return __builtin_amdgcn_readfirstlane((uint32_t)c);
+                    };
+                    const uint32_t cx = cell((float)o.x, qt.mt_lo[0], qt.mt_inv, qt.mt_n[0]);
+                    const uint32_t cy = cell((float)o.y, qt.mt_lo[1], qt.mt_inv, qt.mt_n[1]);
+                    const uint32_t cz = cell((float)o.z, qt.mt_lo[2], qt.mt_inv, qt.mt_n[2]);
+                    ci = 4u * (cx + qt.mt_n[0] * (cy + qt.mt_n[1] * cz));
+                }
+#endif
+#if RT_EXP_TIERS == 4
+#pragma unroll 1
+                for (uint32_t k = ci == 0xFFFFFFFFu ? 3u : 0u; k < 4u; ++k) {
+                    uint64_t w = tm;
+                    if (ci != 0xFFFFFFFFu) {
+                        const auto& qt = *cold_args<T>();
+                        cptr<uint64_t> tt = (cptr<uint64_t>)__builtin_assume_aligned(qt.mtiers, 32);
+                        const uint64_t hi = k < 3u ? tt[ci + k] : ~0ull, lo = k > 0u ? tt[ci + k - 1u] : 0ull;
+                        w = tm & hi & ~lo;
+                    }
+#else
+                uint64_t T0 = 0, T1 = 0;
+                if (ci != 0xFFFFFFFFu) {
+                    const auto& qt = *cold_args<T>();
+                    cptr<uint64_t> tt = (cptr<uint64_t>)__builtin_assume_aligned(qt.mtiers, 32);
+                    T0 = tt[ci];
+                    T1 = RT_EXP_TIERS == 3 ? tt[ci + 1u] : T0;
+                }
+#pragma unroll 1
+                for (uint32_t k = 0; k < 3u; ++k) {
+                    uint64_t w = k == 0u ? tm & T0 : (k == 1u ? tm & T1 & ~T0 : tm & ~T1);
+#endif
+                    while (w != 0ull) {
+                        const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctzll(w);
+                        w &= w - 1ull;
+                        walk_mega(nd);
                     }
                 }
             }
@@ -2250,6 +2311,9 @@ struct rt_context {
     void* lbx64[3] = {}; void* lbx32[3] = {};       // local box levels: cluster boxes, supers, megas
     float l_r2max64 = 0, l_r2min64 = 0, l_r2max32 = 0, l_r2min32 = 0;
     uint32_t n_mg = 0;
+    void* mtiers = nullptr;                         // the mega walk's order table (pack_mega_tiers)
+    float mt_lo[3] = {0, 0, 0}, mt_inv = 0;
+    uint32_t mt_n[3] = {1, 1, 1};
     uint32_t* ridx = nullptr;
     void* clus64 = nullptr; void* clus32 = nullptr;   // cluster bounding spheres {C, R} (double)
     void* cullc64 = nullptr; void* cullc32 = nullptr; // per-cluster camera cull records (rebuilt per launch)
@@ -2355,6 +2419,8 @@ static void free_scene(rt_context* c) {
     }
     c->meg64 = c->meg32 = nullptr;
     c->n_mg = 0;
+    (void)hipFree(c->mtiers);
+    c->mtiers = nullptr;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
     c->clus64 = c->clus32 = c->cullc64 = c->cullc32 = nullptr;
     c->n_cslots = c->n_clp = c->n_supc = 0;
@@ -2727,7 +2793,7 @@ constexpr uint32_t kLBoxFloats = 32;
 template <typename T>
 static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, const std::vector<float>& r2l,
                              std::vector<float>& lclb, std::vector<float>& lsup, std::vector<float>& lmeg,
-                             float& r2max, float& r2min) {
+                             float& r2max, float& r2min, std::vector<float>* wmeg = nullptr) {
     auto up32 = [](double v) -> float {
         float f = (float)v;
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
@@ -2801,6 +2867,7 @@ static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, co
     std::vector<float> wsu, wme;
     unite(wcl, nsup, wsu);
     unite(wsu, nsg, wme);
+    if (wmeg) *wmeg = wme;
     // group-local frames: group g of `world` (4 boxes) -> LBoxGroup g
     auto localise = [&](const std::vector<float>& world, size_t ng, std::vector<float>& out) {
         out.assign((size_t)kLBoxFloats * (ng + 1), 0.0f);
@@ -2845,6 +2912,72 @@ static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, co
     localise(wcl, (nc + 3) / 4, lclb);
     localise(wsu, nsg, lsup);
     localise(wme, (nsg + 3) / 4, lmeg);
+}
+
+// The mega walk's order table (nearest_hit, MEGA): a grid of cubic cells (<= 4096, <= 64 per axis)
+// over the union of the mega boxes (world frame, BoxGroup layout); per cell four u64 masks over the
+// megas (<= 64): those whose box touches the cell, those within a quarter and within a half of the
+// median mega size, and 0 (nested, so the walk's tiers partition the passing megas; the kernel's
+// default uses the first two).  A heuristic:
+// the order changes which boxes get culled early, never the hits.
+struct MegaTiers { std::vector<uint64_t> t; float lo[3] = {0, 0, 0}, inv = 0; uint32_t n[3] = {1, 1, 1}; };
+static MegaTiers pack_mega_tiers(const std::vector<float>& wme, size_t nm) {
+    MegaTiers M;
+    M.t.assign(4, 0ull);
+    if (nm == 0 || nm > 64) return M;
+    std::vector<std::array<double, 6>> bx;
+    std::vector<size_t> id;
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<double> size;
+    for (size_t k = 0; k < nm; ++k) {
+        std::array<double, 6> b;
+        for (int f = 0; f < 6; ++f) b[f] = wme[kBoxFloats * (k / 4) + 12 * ((k % 4) / 2) + 2 * f + (k % 2)];
+        if (!(b[3] > -INFINITY) || !std::isfinite(b[3] + b[4] + b[5] + b[0] + b[1] + b[2])) continue;
+        bx.push_back(b);
+        id.push_back(k);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], b[a] - b[3 + a]);
+            hi[a] = std::max(hi[a], b[a] + b[3 + a]);
+        }
+        size.push_back(2.0 * std::max(b[3], std::max(b[4], b[5])));
+    }
+    if (bx.empty()) return M;
+    std::nth_element(size.begin(), size.begin() + size.size() / 2, size.end());
+    const double L = size[size.size() / 2];
+    double ext = 0.0;
+    for (int a = 0; a < 3; ++a) ext = std::max(ext, hi[a] - lo[a]);
+    double cs = ext > 0.0 ? ext / 64.0 : 1.0;
+    for (;;) {
+        uint64_t prod = 1;
+        for (int a = 0; a < 3; ++a) {
+            M.n[a] = (uint32_t)std::min(64.0, std::max(1.0, std::ceil((hi[a] - lo[a]) / cs)));
+            prod *= M.n[a];
+        }
+        if (prod <= 4096) break;
+        cs *= 1.25;
+    }
+    for (int a = 0; a < 3; ++a) M.lo[a] = (float)lo[a];
+    M.inv = (float)(1.0 / cs);
+    M.t.assign((size_t)4 * M.n[0] * M.n[1] * M.n[2], 0ull);
+    for (uint32_t z = 0; z < M.n[2]; ++z)
+        for (uint32_t y = 0; y < M.n[1]; ++y)
+            for (uint32_t x = 0; x < M.n[0]; ++x) {
+                const double cc[3] = {lo[0] + (x + 0.5) * cs, lo[1] + (y + 0.5) * cs, lo[2] + (z + 0.5) * cs};
+                uint64_t* t = &M.t[(size_t)4 * (x + M.n[0] * (y + M.n[1] * z))];
+                for (size_t j = 0; j < bx.size(); ++j) {
+                    double d2 = 0.0;
+                    for (int a = 0; a < 3; ++a) {
+                        const double g = std::max(0.0, std::fabs(cc[a] - bx[j][a]) - (0.5 * cs + bx[j][3 + a]));
+                        d2 += g * g;
+                    }
+                    const double d = std::sqrt(d2);
+                    const uint64_t bit = 1ull << id[j];
+                    if (d <= 0.0) t[0] |= bit;
+                    if (d <= 0.25 * L) t[1] |= bit;
+                    if (d <= 0.5 * L) t[2] |= bit;
+                }
+            }
+    return M;
 }
 
 extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
@@ -2896,7 +3029,14 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
             pack_local(c32, L, t32, lf32, lr32, q32);
             std::vector<float> b64[3], b32[3];
             pack_local_boxes(c64, L, q64, b64[0], b64[1], b64[2], c->l_r2max64, c->l_r2min64);
-            pack_local_boxes(c32, L, q32, b32[0], b32[1], b32[2], c->l_r2max32, c->l_r2min32);
+            std::vector<float> wme;
+            pack_local_boxes(c32, L, q32, b32[0], b32[1], b32[2], c->l_r2max32, c->l_r2min32, &wme);
+            {
+                const MegaTiers M = pack_mega_tiers(wme, (L.members.size() / 4 + 3) / 4);
+                if ((rc = up(&c->mtiers, M.t.data(), M.t.size() * sizeof(uint64_t))) != RT_OK) return rc;
+                for (int a = 0; a < 3; ++a) { c->mt_lo[a] = M.lo[a]; c->mt_n[a] = M.n[a]; }
+                c->mt_inv = M.inv;
+            }
             for (int lv = 0; lv < 3; ++lv) {
                 if ((rc = up(&c->lbx64[lv], b64[lv].data(), b64[lv].size() * sizeof(float))) != RT_OK) return rc;
                 if ((rc = up(&c->lbx32[lv], b32[lv].data(), b32[lv].size() * sizeof(float))) != RT_OK) return rc;
@@ -3062,6 +3202,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.lclb = (const float*)(f64 ? c->lbx64[0] : c->lbx32[0]);
     p.lsup = (const float*)(f64 ? c->lbx64[1] : c->lbx32[1]);
     p.lmeg = (const float*)(f64 ? c->lbx64[2] : c->lbx32[2]);
+    p.mtiers = (const uint64_t*)c->mtiers;
+    for (int a = 0; a < 3; ++a) { p.mt_lo[a] = c->mt_lo[a]; p.mt_n[a] = c->mt_n[a]; }
+    p.mt_inv = c->mt_inv;
     {
         auto up32 = [](double v) -> float {
             float f = (float)v;

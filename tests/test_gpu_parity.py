@@ -300,6 +300,15 @@ def test_config_e_scene(renderer, flags, spp):
     assert_parity(renderer, flat, cam_for(4, 3), 50, spp, flags)
 
 
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_F32, 0])
+def test_more_than_64_megas(renderer, flags):
+    """70 000 spheres: 274 mega boxes, more than the 64 the mega walk tests at once (and orders by the
+    host's distance tiers), so the sweep walks them in chunks of 32 in index order."""
+    flat = rt.scenes.random_spheres(70000).flatten()
+    assert flat.n_spheres == 70000
+    assert_parity(renderer, flat, cam_for(4, 3), 50, 32, flags)
+
+
 # ---- semantics modes (tests/test_modes.py pins them on the CPU) ----
 MODES = [abi.RT_FLAG_MODE_VECTORIZED, abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_ROOT2, abi.RT_FLAG_MODE_SCALAR,
          abi.RT_FLAG_MODE_VECTORIZED3, abi.RT_FLAG_MODE_VECTORIZED3 | abi.RT_FLAG_ROOT2]
