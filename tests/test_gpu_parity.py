@@ -301,11 +301,13 @@ def test_config_e_scene(renderer, flags, spp):
 
 
 @pytest.mark.parametrize("flags", [abi.RT_FLAG_F32, 0])
-def test_more_than_64_megas(renderer, flags):
-    """70 000 spheres: 274 mega boxes, more than the 64 the mega walk tests at once (and orders by the
-    host's distance tiers), so the sweep walks them in chunks of 32 in index order."""
-    flat = rt.scenes.random_spheres(70000).flatten()
-    assert flat.n_spheres == 70000
+@pytest.mark.parametrize("n", [3000, 70000])
+def test_mega_walk_shapes(renderer, flags, n):
+    """The mega kernels' top level in its other shapes (config E: 40 megas in 10 groups, walked in
+    distance tiers).  3 000 spheres: 12 megas in 3 groups.  70 000: 274 megas in 69 groups, more than
+    the 16 the walk tests at once, so chunks of 8 groups in index order."""
+    flat = rt.scenes.random_spheres(n).flatten()
+    assert flat.n_spheres == n
     assert_parity(renderer, flat, cam_for(4, 3), 50, 32, flags)
 
 
