@@ -938,23 +938,22 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             // whose box touches the cell, then those within a quarter and a half of a mega's size,
             // then the rest), index order inside a tier.  More megas: chunks of 32 in index order.
             const uint32_t span = ntg <= 16u ? 16u : 8u;
+#ifndef RT_EXP_KTEST
+#define RT_EXP_KTEST 1
+#endif
+            constexpr uint32_t kTest = RT_EXP_KTEST;   // the tiers below kTest are walked before the top-level tests
             for (uint32_t t0 = 0; t0 < ntg; t0 += span) {
                 const uint32_t nt = min(span, ntg - t0);
-                uint64_t tm = 0;
-                n_box += nt;
-                for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
-                    lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
-                        KSTAT(5);
-                        tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
-                    });
-                if (4u * (t0 + nt) > nsg) tm &= (1ull << (nsg - 4u * t0)) - 1ull;   // padding megas (empty boxes)
-#ifndef RT_EXP_TIERS
-#define RT_EXP_TIERS 3
-#endif
-                // RT_EXP_TIERS 3 (default): T0 and T1 held in SGPRs, T2 merged into the rest; 4: all four
-                // tiers, each mask re-read per tier (scalar loads); 2: T0 only.  Same-box E fp32: 9819 /
-                // 9773 / 9794, against 9328 in index order (profiles/r02/experiments/tiers.txt)
-                uint32_t ci = 0xFFFFFFFFu;   // the reference cell's table row (none: one tier)
+                // padding megas (empty boxes) past the last
+                const uint64_t valid = 4u * (t0 + nt) > nsg ? (1ull << (nsg - 4u * t0)) - 1ull : ~0ull;
+                // Tiers (span 16, up to 64 megas): T0 = the megas whose box touches the reference point's
+                // grid cell (the first active lane's origin), T1 = those within a quarter of a mega's
+                // size (the host's table, pack_mega_tiers); the tier-0 megas are walked first without
+                // a top-level test (a mega the rays miss has no passing supers either), then all mega
+                // boxes are tested, with the best hits found so far culling far ones, and the rest are
+                // walked tier by tier, index order inside a tier.  Same-box E fp32: 9328 in index order,
+                // 9819 with the tiers (profiles/r02/experiments/tiers.txt, tiers_t0.txt)
+                uint64_t T0 = 0, T1 = 0;
 #if !defined(RT_EXP_NO_ORDER)
                 if (span == 16u) {
                     const auto& qt = *cold_args<T>();
@@ -965,31 +964,26 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     const uint32_t cx = cell((float)o.x, qt.mt_lo[0], qt.mt_inv, qt.mt_n[0]);
                     const uint32_t cy = cell((float)o.y, qt.mt_lo[1], qt.mt_inv, qt.mt_n[1]);
                     const uint32_t cz = cell((float)o.z, qt.mt_lo[2], qt.mt_inv, qt.mt_n[2]);
-                    ci = 4u * (cx + qt.mt_n[0] * (cy + qt.mt_n[1] * cz));
+                    const uint32_t ci = 4u * (cx + qt.mt_n[0] * (cy + qt.mt_n[1] * cz));
+                    cptr<uint64_t> tt = (cptr<uint64_t>)__builtin_assume_aligned(qt.mtiers, 32);
+                    T0 = tt[ci] & valid;
+                    T1 = tt[ci + 1u] & valid;
                 }
 #endif
-#if RT_EXP_TIERS == 4
-#pragma unroll 1
-                for (uint32_t k = ci == 0xFFFFFFFFu ? 3u : 0u; k < 4u; ++k) {
-                    uint64_t w = tm;
-                    if (ci != 0xFFFFFFFFu) {
-                        const auto& qt = *cold_args<T>();
-                        cptr<uint64_t> tt = (cptr<uint64_t>)__builtin_assume_aligned(qt.mtiers, 32);
-                        const uint64_t hi = k < 3u ? tt[ci + k] : ~0ull, lo = k > 0u ? tt[ci + k - 1u] : 0ull;
-                        w = tm & hi & ~lo;
-                    }
-#else
-                uint64_t T0 = 0, T1 = 0;
-                if (ci != 0xFFFFFFFFu) {
-                    const auto& qt = *cold_args<T>();
-                    cptr<uint64_t> tt = (cptr<uint64_t>)__builtin_assume_aligned(qt.mtiers, 32);
-                    T0 = tt[ci];
-                    T1 = RT_EXP_TIERS == 3 ? tt[ci + 1u] : T0;
-                }
+                uint64_t tm = 0;
 #pragma unroll 1
                 for (uint32_t k = 0; k < 3u; ++k) {
-                    uint64_t w = k == 0u ? tm & T0 : (k == 1u ? tm & T1 & ~T0 : tm & ~T1);
-#endif
+                    if (k == kTest) {
+                        n_box += nt;
+                        for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
+                            lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
+                                KSTAT(5);
+                                tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
+                            });
+                        tm &= valid;
+                    }
+                    uint64_t w = k == 0u ? (kTest == 0u ? tm & T0 : T0)
+                                         : (k == 1u ? (kTest <= 1u ? tm & T1 : T1) & ~T0 : tm & ~T1);
                     while (w != 0ull) {
                         const uint32_t nd = 4u * t0 + (uint32_t)__builtin_ctzll(w);
                         w &= w - 1ull;
