@@ -20,7 +20,11 @@ roofline: the trace kernel is bound by VALU issue (no MFMA; HBM 
   per ray segment and sphere) is reported separately as brute_force_equiv: the culls
   skip most of it, so its "rate" exceeds the chip's peak and says how much work is avoided.
   valu_busy and traffic come from rocprofv3 PMC passes of this bench (profiles/pmc.json, with the
-  commit they were collected at).
+  commit and kernel-source hash they were collected at); when that hash is not the loaded library's
+  (rt_version() "src=..."), they are reported as null and pmc_source.stale = true.
+--gpus N > 1 without a launcher (no RANK in the environment): bench.py starts N ranks itself, as a
+  child `python -m torch.distributed.run --nproc-per-node N bench.py ...` (never exec), and exits with
+  its return code; a rank whose initialised world size is not --gpus exits non-zero.
 cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>), built
   -march=native on this host, on every core this process may use (affinity, capped by the cgroup's
   CPU quota), over a bounded strided pixel sample of the same workload.
@@ -29,6 +33,8 @@ import argparse
 import ctypes
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -52,7 +58,39 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc.json"))
     ap.add_argument("--max-spheres", type=int, default=0, help="experiment: truncate the scene (not a bench line)")
+    ap.add_argument("--probe-dist", action="store_true",
+                    help="launcher rehearsal: set up the ranks and the process group, print the world, no GPU work")
     return ap.parse_args()
+
+
+def pmc_fields(pmc, lib_src_hash, source_file):
+    """roofline.traffic / valu_busy / pmc_source from a PMC record (tools/pmc_round.py).  The figures
+    count only if they were collected from the kernel sources the loaded library was built from:
+    otherwise (another hash, or a record without one) they are null and pmc_source.stale is true."""
+    if not pmc:
+        return {"traffic": None, "valu_busy": None, "pmc_source": None}
+    stale = pmc.get("src_hash") is None or pmc.get("src_hash") != lib_src_hash
+    return {"traffic": None if stale else pmc.get("hbm_bytes_per_launch"),
+            "valu_busy": None if stale else pmc.get("valu_busy"),
+            "pmc_source": {"file": source_file, "commit": pmc.get("commit"), "src_hash": pmc.get("src_hash"),
+                           "library_src_hash": lib_src_hash, "stale": stale, "launch_ms": pmc.get("launch_ms")}}
+
+
+def self_launch(args):
+    """--gpus N > 1 with no launcher around us: run N ranks under torch.distributed.run as a child
+    process (one process per GPU, rendezvous on 127.0.0.1) and return its exit code; None when this
+    process is already a rank (or N == 1).  Nothing here touches the GPU."""
+    if args.gpus <= 1 or "RANK" in os.environ or "WORLD_SIZE" in os.environ:
+        return None
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    print(f"bench.py: --gpus {args.gpus}: launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
 
 
 def cpu_share():
@@ -118,11 +156,12 @@ def cpu_baseline(flat, cam, depth, spp, seed, budget_s, threads, host):
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
 
     import numpy as np
     import torch   # imported before the HIP library so both share one HIP runtime
@@ -131,8 +170,10 @@ def main():
     # One process per GPU.  RT_BENCH_BACKEND=gloo (rehearsal only: several ranks sharing one GPU,
     # shards staged through host memory) exercises the same partition/gather/assembly code.
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
-    device = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(device)
+    device = 0
+    if not args.probe_dist:
+        device = local_rank % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(device)
     if world > 1 or "RANK" in os.environ:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
@@ -140,11 +181,35 @@ def main():
             dist.init_process_group(backend)
     dist_on = dist.is_initialized()
     world_init = dist.get_world_size() if dist_on else 1
+    if world_init != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the initialised world size is {world_init} "
+              f"(WORLD_SIZE={os.environ.get('WORLD_SIZE')}): refusing to report a {world_init}-GPU line as "
+              f"{args.gpus} GPUs", file=sys.stderr, flush=True)
+        sys.exit(3)
+    if args.probe_dist:
+        ranks = [rank]
+        if dist_on:
+            t = torch.tensor([float(rank)], dtype=torch.float64)
+            allr = [torch.empty_like(t) for _ in range(world_init)]
+            dist.all_gather(allr, t)
+            ranks = [int(a.item()) for a in allr]
+        if rank == 0:
+            print(json.dumps({"probe_dist": True, "n_gpus": world_init, "gpus_arg": args.gpus,
+                              "dist": {"backend": backend if dist_on else None, "world_size_initialised": world_init,
+                                       "ranks": ranks}}), flush=True)
+        if dist_on:
+            dist.destroy_process_group()
+        return
 
     import rt_mi355x as rt
     from rt_mi355x import abi
 
     lib = rt.load_library()
+    vinfo = abi.version_info(lib)
+    src_hash = abi.source_hash()
+    if vinfo["src_hash"] != src_hash and rank == 0:
+        print(f"bench.py: warning: the library was built from sources {vinfo['src_hash']}, the tree holds "
+              f"{src_hash} (rebuild with make -C rust-ray-tracing_amd)", file=sys.stderr, flush=True)
     W, H, n_sph, spp, depth = rt.scenes.CONFIGS[args.config]
     scene = rt.scenes.config_scene(args.config)
     if args.max_spheres:
@@ -274,12 +339,9 @@ def main():
         except (OSError, ValueError):
             pass
         rl = head["roofline"]
-        rl["traffic"] = pmc.get("hbm_bytes_per_launch")
+        rl.update(pmc_fields(pmc, vinfo["src_hash"], os.path.relpath(args.pmc, REPO)))
         rl["algorithmic_bytes"] = tile.row_count * W * 3 + flat.n_spheres * 20   # RGB8 out + the scene (SoA)
         rl["traffic_over_algorithmic"] = (rl["traffic"] / rl["algorithmic_bytes"]) if rl["traffic"] else None
-        rl["valu_busy"] = pmc.get("valu_busy")
-        rl["pmc_source"] = ({"file": os.path.relpath(args.pmc, REPO), "commit": pmc.get("commit"),
-                             "launch_ms": pmc.get("launch_ms")} if pmc else None)
         line = {
             "metric": "Msamples/s (pixels×spp/s), 1920×1080·512spp·500 spheres; 1/2/4/8 GPU",
             "value": round(head["value"], 3),
@@ -315,13 +377,17 @@ def main():
                         "achieved_tflops": round(o["roofline"]["achieved"], 3),
                         "brute_force_equiv_tflops": round(o["roofline"]["brute_force_equiv"]["tflops"], 3),
                         "range_error": o["range_error"]}
+        rms = [p[1] for p in head["per_rank"]]
         line["dist"] = {
             "backend": (backend if dist_on else None), "world_size_initialised": world_init,
+            "imbalance": round(max(rms) / (sum(rms) / len(rms)), 4) if sum(rms) > 0 else None,   # max / mean render
             "rccl_version": (".".join(map(str, torch.cuda.nccl.version())) if dist_on and backend == "nccl" else None),
             "per_rank": [{"rank": r, "wall_s": round(p[0], 4), "render_ms": round(p[1], 3), "gather_ms": round(p[2], 3),
                           "assemble_ms": round(p[3], 3), "ray_segments": int(p[4]), "px_per_s": round(p[5], 1)}
                          for r, p in enumerate(head["per_rank"])],
         }
+        line["build"] = {"library": vinfo["version"], "source_hash": src_hash,
+                         "library_matches_source": vinfo["src_hash"] == src_hash}
         if world == 1 and args.cpu_seconds > 0:
             threads, host = cpu_share()
             threads = args.cpu_threads or threads

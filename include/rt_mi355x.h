@@ -171,7 +171,7 @@ int rt_memcpy_d2h(rt_context* ctx, void* dst, const void* src, size_t bytes);   
 
 /* Last error message of the calling thread ("" if none). */
 const char* rt_last_error(void);
-/* Build/version string, e.g. "rt_mi355x 0.1 gfx950". */
+/* Build/version string: "rt_mi355x <version> gfx950 <product|experiment> src=<source hash>". */
 const char* rt_version(void);
 
 #ifdef __cplusplus

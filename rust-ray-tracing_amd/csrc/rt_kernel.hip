@@ -46,6 +46,31 @@
 #include "../../include/rt_mi355x.h"
 #include "rt_device.hpp"
 
+// Build kinds.  The product library (make) defines RT_PRODUCT and refuses every experiment macro
+// below; the A/B builds (make exp / kstats) define RT_EXPERIMENT, and rt_version() says so, which
+// rt_mi355x.load_library refuses unless RT_ALLOW_EXPERIMENT=1.  Every experiment keeps the results
+// bit-identical (timing or ordering changes only); tests/test_abi.py checks that this list names
+// every RT_EXP_ macro the source tests.
+#if defined(RT_PRODUCT) && defined(RT_EXPERIMENT)
+#error "RT_PRODUCT and RT_EXPERIMENT are exclusive"
+#endif
+#if defined(RT_PRODUCT) && (defined(RT_EXP_FLAT_SWEEP) || defined(RT_EXP_NO_PRUNE) || defined(RT_EXP_NO_XREC) ||   \
+                            defined(RT_EXP_KTEST) || defined(RT_EXP_NO_ORDER) || defined(RT_EXP_SLOTS) ||            \
+                            defined(RT_EXP_BLOCK_SAMPLES) || defined(RT_EXP_TMUL) || defined(RT_EXP_OLD_REPLAY) ||   \
+                            defined(RT_EXP_NO_PARK) || defined(RT_EXP_PARKC_ALL) || defined(RT_EXP_DUP_FINISH) ||    \
+                            defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
+                            defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_KSTATS))
+#error "an experiment macro in the product build"
+#endif
+#ifndef RT_SRC_HASH
+#define RT_SRC_HASH "unknown"
+#endif
+#ifdef RT_EXPERIMENT
+#define RT_BUILD_KIND "experiment"
+#else
+#define RT_BUILD_KIND "product"
+#endif
+
 namespace rt {
 
 template <typename T> struct MatT {
@@ -185,11 +210,13 @@ enum WorkCounter : uint32_t {
 };
 constexpr int kWorkSlot = 11;   // shard slots 11..15 (kstats uses 3..10)
 static_assert(kWorkSlot + kNWork <= kSegStride, "work counters past the shard's line");
-__shared__ uint32_t g_work[4][kNWork];
+// u64: a wave of a persistent launch can run billions of tests (config E: ~1.3M filter groups per
+// wave; spp up to 2^20 on a 4K frame is ~3000x that), past a u32.
+__shared__ unsigned long long g_work[4][kNWork];
 // Add wave-uniform counts from the first active lane (the caller may be inside a divergent branch).
 __device__ __forceinline__ void work_add(uint32_t i, uint32_t n) {
     const uint32_t first = (uint32_t)__builtin_ctzll(__builtin_amdgcn_read_exec());
-    if ((threadIdx.x & 63u) == first) atomicAdd(&g_work[threadIdx.x >> 6][i], n);
+    if ((threadIdx.x & 63u) == first) atomicAdd(&g_work[threadIdx.x >> 6][i], (unsigned long long)n);
 }
 
 // Instrumented build only (make kstats): wave-level event counters, written to shard slots 3..10.
@@ -1527,16 +1554,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
-#ifdef RT_EXP_SKIP_REDUCE
-constexpr bool kSkipReduce = true;
-#else
-constexpr bool kSkipReduce = false;
-#endif
-#ifdef RT_EXP_SKIP_INIT
-constexpr bool kSkipInit = true;   // timing experiment only: results are wrong
-#else
-constexpr bool kSkipInit = false;
-#endif
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
                                                  T (*stage)[64]) {
@@ -1548,7 +1565,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // Map init: no position holds a terminated sample's value yet (survivors and never-written
     // positions read 0; positions [spp, P), the missing lanes of a partial last chunk, get their
     // fixed value in the final reduction).  Two u16 entries per u32 store.
-    if (MODE == kModeV2 && !kSkipInit) {
+    if (MODE == kModeV2) {
         if (sc.wide & 2u) {
             for (uint32_t qi = lane; qi < P; qi += 64u) sc.set_map(qi, kNone);
         } else {
@@ -1591,7 +1608,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // the retire rule then picks which of the two holds its value, and the position
     // map records the sample there (the value itself is formed in the final reduction).
     bool replayed = false;
-#if !defined(RT_EXP_SKIP_REPLAY) && !defined(RT_EXP_OLD_REPLAY)
+#if !defined(RT_EXP_OLD_REPLAY)
     if (MODE == kModeV2 && K > 0u && K <= 64u) {
         replayed = true;
         const uint32_t H = hist[lane];
@@ -1617,9 +1634,6 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const bool in = i < spp, ret = e < K;
                 unsigned long long rem = __ballot(ret);
                 uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nk = 0, nn = 0;
-#ifdef RT_EXP_NO_POSLOOP   // timing experiment only: results are wrong
-                rem = 0ull; pold = i; pnew = i;
-#endif
                 while (rem != 0ull) {   // one pass per distinct bounce k among the chunk's retiring lanes
                     const uint32_t k = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(rem));
                     const unsigned long long bge = __ballot(in && e >= k), beq = __ballot(e == k);
@@ -1639,11 +1653,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 cge += gadd + (uint32_t)__popcll(__ballot(in && e >= K));
                 ceq += hc;
                 const uint32_t ek = ret ? e : 0u;
-#ifdef RT_EXP_NO_RWRITES   // timing experiment only: results are wrong
-                if (ret && pold == 0xFFFFFFFFu) {
-#else
                 if (ret) {
-#endif
                     const uint32_t Lk = (nk + 3u) / 4u, Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
                     const uint32_t lo = 4u * Lnext, hi = 4u * Lk;   // positions retiring at bounce e
                     const bool U = q.s_sel == (ek & 1u);
@@ -1720,11 +1730,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         }
     }
     uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
-#ifdef RT_EXP_SKIP_REPLAY
-    for (uint32_t k = 0; k < 0u; ++k) {   // timing experiment only: results are wrong
-#else
     for (uint32_t k = 0; k < (MODE == kModeV2 && !replayed ? K : 0u); ++k) {
-#endif
         if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
             kb = k;
             hist[lane] = 0;
@@ -1777,11 +1783,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // over each sample's own value (+0 for the disabled lanes of a partial chunk: black x sky).
     // Scalar: Color::average (color.rs:66-85), one sequential sum over the samples.
     T acc = T(0.0);
-#ifdef RT_EXP_SKIP_REDUCE   // timing experiment only: results are wrong
-    if (false) {
-#else
     if (MODE == kModeScalar) {
-#endif
         if (lane < 3u) {
             uint32_t i = 0;
             for (; i + 16 <= spp; i += 16) {
@@ -1796,7 +1798,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             }
             for (; i < spp; ++i) acc = acc + (&sc.c(s, i).x)[lane];
         }
-    } else if (!kSkipReduce) {
+    } else {
         const V3<T> s0 = sky(T(0.0));
         const bool white0 = depth == 0u && q.s_sel == 0u;
         // the 12 running sums live in LDS (the free histogram) between batches: a short live range
@@ -1891,7 +1893,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     constexpr bool SC = MODE == kModeScalar;
     constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? kQCap : 1;
     __shared__ unsigned long long wcount[4][3];
-    __shared__ uint32_t s_hist[4][64];
+    // 8-byte aligned: finish_pixel keeps its 12 running sums (T, fp64 too) in this array
+    __shared__ __attribute__((aligned(16))) uint32_t s_hist[4][64];
     __shared__ __attribute__((aligned(16))) T s_stage[4][3][64];   // finish_pixel: 64 positions' values per wave
     __shared__ IssueState s_is[4];
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
@@ -1917,7 +1920,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
-    if (lane < kNWork) g_work[wave][lane] = 0u;
+    if (lane < kNWork) g_work[wave][lane] = 0ull;
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
@@ -2037,15 +2040,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                          const V3<T>& td) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
-#ifndef RT_EXP_NO_EWRITE   // traffic experiment only: results are wrong
             sc.set_e(t_slot, t_sid, e);
-#endif
             if (MODE == kModeV2) {
                 // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
                 // the copies into them raised the register peak (spills in the sphere sweeps)
-#ifndef RT_EXP_NO_CWRITE   // traffic experiment only: results are wrong
                 if (skyhit) sc.store_c(t_slot, t_sid, tc.x, tc.y, tc.z);
-#endif
             } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
                 V3<T> v = mk(T(0.0), T(0.0), T(0.0));
                 if (skyhit) { const V3<T> sk = sky(td.y); v = mk(tc.x * sk.x, tc.y * sk.y, tc.z * sk.z); }
@@ -2113,9 +2112,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const V3<T> vu = mk(q.vu[0], q.vu[1], q.vu[2]), vv = mk(q.vv[0], q.vv[1], q.vv[2]);
             const V3<T> pc = add(mk(q.ulc[0], q.ulc[1], q.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
             bd = unit(sub(pc, mk(q.center[0], q.center[1], q.center[2])));
-#ifndef RT_EXP_NO_YWRITE   // traffic experiment only: results are wrong
             if (MODE == kModeV2) wave_scratch<T>(wave).y(bslot, bsid) = bd.y;   // primary y (quirk Q2)
-#endif
         }
         T bt = T(0);
         int bi = -1;
@@ -2212,9 +2209,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (fresh) {
             k = 0;
             live = true;
-#ifndef RT_EXP_NO_YWRITE   // traffic experiment only: results are wrong
             if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
-#endif
         } else if (scat) {
             k += 1u;
         }
@@ -2255,7 +2250,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         atomicAdd(cc + 0, wcount[wave][0]);
         atomicAdd(cc + 1, wcount[wave][1]);
         atomicAdd(cc + 2, wcount[wave][2]);
-        for (uint32_t i = 0; i < kNWork; ++i) atomicAdd(cc + kWorkSlot + i, (unsigned long long)g_work[wave][i]);
+        for (uint32_t i = 0; i < kNWork; ++i) atomicAdd(cc + kWorkSlot + i, g_work[wave][i]);
 #ifdef RT_KSTATS
         for (int i = 0; i < 8; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);
 #endif
@@ -2330,7 +2325,8 @@ struct rt_context {
 };
 
 extern "C" const char* rt_last_error(void) { return g_err.c_str(); }
-extern "C" const char* rt_version(void) { return "rt_mi355x 0.1 gfx950"; }
+// "rt_mi355x <version> gfx950 <product|experiment> src=<hash of the sources it was built from>"
+extern "C" const char* rt_version(void) { return "rt_mi355x 0.3 gfx950 " RT_BUILD_KIND " src=" RT_SRC_HASH; }
 
 extern "C" double rt_metal_clamp_fuzz(double fuzz) { return fuzz < 1.0 ? fuzz : 1.0; }
 

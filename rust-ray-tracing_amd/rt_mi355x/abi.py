@@ -4,6 +4,7 @@ The structures below are shared by the product library (lib/librt_mi355x.so) and
 test-only oracle (oracle/build/liboracle.so), whose structs have the same layout.
 """
 import ctypes
+import hashlib
 import os
 
 u32 = ctypes.c_uint32
@@ -95,9 +96,31 @@ EXPORTED = [
 
 _lib = None
 
+# The sources the Makefile hashes into rt_version() ("src=<hash>"), in its order.
+SOURCE_FILES = [os.path.join(PKG_DIR, "csrc", "rt_kernel.hip"), os.path.join(PKG_DIR, "csrc", "rt_device.hpp"),
+                os.path.join(os.path.dirname(PKG_DIR), "include", "rt_mi355x.h")]
+
+
+def source_hash():
+    """sha256 (first 12 hex digits) of the kernel sources, as the Makefile computes it."""
+    h = hashlib.sha256()
+    for f in SOURCE_FILES:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def version_info(lib):
+    """rt_version() parsed: {"version": str, "kind": "product" | "experiment" | None, "src_hash": str | None}."""
+    v = lib.rt_version().decode()
+    kind = "experiment" if " experiment" in v else ("product" if " product" in v else None)
+    src = v.split("src=", 1)[1].split()[0] if "src=" in v else None
+    return {"version": v, "kind": kind, "src_hash": src}
+
 
 def load_library(path=None):
-    """Load the product library.  Raises (never falls back) when it has not been built."""
+    """Load the product library.  Raises (never falls back) when it has not been built, and refuses an
+    experiment build (make exp / kstats) unless RT_ALLOW_EXPERIMENT=1 (same-box A/B scripts only)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -105,6 +128,10 @@ def load_library(path=None):
     if not os.path.exists(p):
         raise RuntimeError(f"rt_mi355x: HIP library not built: {p} (run `make -C rust-ray-tracing_amd`)")
     lib = ctypes.CDLL(p)
+    lib.rt_version.restype = ctypes.c_char_p
+    if version_info(lib)["kind"] == "experiment" and os.environ.get("RT_ALLOW_EXPERIMENT") != "1":
+        raise RuntimeError(f"rt_mi355x: {p} is an experiment build ({lib.rt_version().decode()}); "
+                           "set RT_ALLOW_EXPERIMENT=1 for A/B runs")
     P = ctypes.POINTER
     vp = ctypes.c_void_p
     lib.rt_camera_new.argtypes = [P(RtCamera), u32, u32, f64, f64, P(f64), P(f64), P(f64), f64]

@@ -82,6 +82,9 @@ class GpuRenderer(Renderer):
             pass
 
     def set_scene(self, flat):
+        # rt_context_set_scene frees the previous scene before uploading this one: if the upload fails
+        # the context holds no usable scene, so the cache must not point at the previous one either.
+        self._scene_flat = None
         abi.check(self.lib, self.lib.rt_context_set_scene(self.ctx, ctypes.byref(flat.abi)))
         # A strong reference, compared with `is`: an id() key could match a new FlatScene that CPython
         # allocated at a freed one's address, and the render would silently use the old spheres.

@@ -130,3 +130,57 @@ def test_header_constants_match_python_mirror():
             "RT_FLAG_ALL"} <= set(defs)
     for name, val in defs.items():
         assert getattr(abi, name) == int(val, 0), name
+
+
+# ---- build kinds (product vs experiment) and the source hash -------------------------------------
+KERNEL = os.path.join(REPO, "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")
+MAKEFILE = os.path.join(REPO, "rust-ray-tracing_amd", "Makefile")
+
+
+def test_product_library_reports_its_sources():
+    """The default build is a product build, made from the sources in this tree."""
+    _ensure_built()
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    lib.rt_version.restype = ctypes.c_char_p
+    v = abi.version_info(lib)
+    assert v["kind"] == "product", v
+    assert v["src_hash"] == abi.source_hash(), (v, "rebuild: make -C rust-ray-tracing_amd")
+
+
+def test_every_experiment_macro_is_refused_by_the_product_build():
+    """Each RT_EXP_* (and RT_KSTATS) macro the kernel tests is in the #error list the product build
+    (-DRT_PRODUCT) checks, and the product rule defines RT_PRODUCT and no experiment macro."""
+    src = open(KERNEL).read()
+    guard = src[src.index("#if defined(RT_PRODUCT) && (defined("):]
+    guard = guard[:guard.index("#error")]
+    listed = set(re.findall(r"defined\((RT_EXP_\w+|RT_KSTATS)\)", guard))
+    used = set(re.findall(r"#\s*(?:ifdef|ifndef|if\s+!?\s*defined\(|elif\s+defined\()\s*(RT_EXP_\w+|RT_KSTATS)", src))
+    used |= set(re.findall(r"defined\((RT_EXP_\w+)\)", src))
+    assert used and used <= listed, sorted(used - listed)
+    mk = open(MAKEFILE).read()
+    rule = mk[mk.index("$(LIB): $(SRC) $(HDR)"):].split("\n\n")[0]
+    assert "-DRT_PRODUCT" in rule and "RT_EXP" not in rule and "RT_EXPERIMENT" not in rule
+    assert "RT_EXP" not in mk.split("HIPFLAGS ?=")[1].split("\n")[0]
+
+
+def test_experiment_library_is_refused(tmp_path):
+    """rt_mi355x.load_library refuses a library whose rt_version() says "experiment" (make exp / kstats)
+    unless RT_ALLOW_EXPERIMENT=1.  A stand-in .so with only rt_version() is enough to check the gate."""
+    c = tmp_path / "fake.c"
+    c.write_text('const char* rt_version(void) { return "rt_mi355x 0.3 gfx950 experiment src=000000000000"; }\n')
+    so = tmp_path / "libfake.so"
+    subprocess.run(["gcc", "-shared", "-fPIC", "-o", str(so), str(c)], check=True)
+    old = os.environ.pop("RT_ALLOW_EXPERIMENT", None)
+    try:
+        with pytest.raises(RuntimeError, match="experiment build"):
+            abi.load_library(str(so))
+    finally:
+        if old is not None:
+            os.environ["RT_ALLOW_EXPERIMENT"] = old
+
+
+def test_source_hash_matches_the_makefile_recipe():
+    """abi.source_hash() == `cat kernel device-header abi-header | sha256sum | cut -c1-12`."""
+    out = subprocess.run("cat " + " ".join(abi.SOURCE_FILES) + " | sha256sum | cut -c1-12", shell=True,
+                         capture_output=True, text=True, check=True).stdout.strip()
+    assert out == abi.source_hash()

@@ -10,7 +10,7 @@ for i in $(seq 1 $R); do
   for V in "$@"; do
     N=${V%@*}; W=""; [ "$V" != "$N" ] && W=${V#*@}
     LIB=""; [ "$N" != base ] && LIB=$PWD/rust-ray-tracing_amd/lib/librt_mi355x_$N.so
-    RT_WAVES=$W RT_MI355X_LIB=$LIB timeout -k 10 120 python bench.py --config $CFG --cpu-seconds 0 --steps 3 \
+    RT_WAVES=$W RT_ALLOW_EXPERIMENT=1 RT_MI355X_LIB=$LIB timeout -k 10 120 python bench.py --config $CFG --cpu-seconds 0 --steps 3 \
         --other-precision 0 --precision $PREC > gpurun_out/ab/${PREC}_${CFG}_${V}_$i.log 2>&1
   done
 done

@@ -6,7 +6,7 @@ PREC=${1:-f32}; R=${2:-3}
 for i in $(seq 1 $R); do
   for L in base exp; do
     LIB=""; [ $L = exp ] && LIB=$PWD/rust-ray-tracing_amd/lib/librt_mi355x_exp.so
-    RT_MI355X_LIB=$LIB timeout -k 10 120 python bench.py --cpu-seconds 0 --steps 3 --precision $PREC > gpurun_out/abx_${PREC}_${L}_$i.log 2>&1
+    RT_ALLOW_EXPERIMENT=1 RT_MI355X_LIB=$LIB timeout -k 10 120 python bench.py --cpu-seconds 0 --steps 3 --precision $PREC > gpurun_out/abx_${PREC}_${L}_$i.log 2>&1
   done
 done
 python3 - "$PREC" "$R" <<'PY'

@@ -19,6 +19,10 @@ import os
 import subprocess
 import sys
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "rust-ray-tracing_amd"))
+from rt_mi355x import abi  # noqa: E402  (source_hash: no GPU needed)
+
 out, key = sys.argv[1], sys.argv[2]
 N_SIMD = 1024
 
@@ -47,9 +51,13 @@ def busy_ratio(d):
     return d["SQ_ACTIVE_INST_VALU"] / (N_SIMD * d["GRBM_GUI_ACTIVE"] / 8.0)
 
 
+# The GPU box has no .git: the caller passes the commit in RT_COMMIT (expanded where the tree was sent
+# from); the source hash is what bench.py checks (the library's rt_version() carries the same hash).
+commit = os.environ.get("RT_COMMIT") or subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True,
+                                                        text=True, cwd=REPO).stdout.strip() or None
 rec = {
-    "commit": subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True,
-                             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__)))).stdout.strip() or None,
+    "commit": commit,
+    "src_hash": abi.source_hash(),
     "kernel": sq["_k"],
     "launch_ms": sq["_t"] * 1e3,
     "fetch_bytes_raw": fetch["FETCH_SIZE"] * 1024,

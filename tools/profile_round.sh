@@ -25,7 +25,12 @@ pass() {   # name, counters, command...
 pass pmc_fetch FETCH_SIZE python3 bench.py $ARGS || exit 1
 pass pmc_write WRITE_SIZE python3 bench.py $ARGS || exit 1
 pass pmc_sq "$SQ" python3 bench.py $ARGS || exit 1
-if [ -x tools/bin/ubench_valu ]; then pass ubench_sq "$SQ" ./tools/bin/ubench_valu || exit 1; fi
+# the VALU issue ceiling (valu_busy's denominator): built here if this tree has no binary
+if [ ! -x tools/bin/ubench_valu ]; then
+  mkdir -p tools/bin && /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -o tools/bin/ubench_valu tools/ubench_valu.hip \
+      || { echo "ubench_valu build failed: no valu_busy" >> "$OUT/status.txt"; exit 1; }
+fi
+pass ubench_sq "$SQ" ./tools/bin/ubench_valu || exit 1
 python3 tools/pmc_round.py "$OUT" "$CFG:$PREC:1" > "$OUT/pmc_summary.txt" 2>&1 || exit 1
 timeout -k 10 300 python3 bench.py --config "$CFG" --precision "$PREC" --steps 10 --warmup 2 --pmc "$OUT/pmc.json" \
     > "$OUT/bench.log" 2>&1 || exit 1

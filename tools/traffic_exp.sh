@@ -10,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for V in "$@"; do
   LIB=""; [ "$V" != base ] && LIB=$PWD/rust-ray-tracing_amd/lib/librt_mi355x_$V.so
   for C in FETCH_SIZE WRITE_SIZE; do
-    RT_MI355X_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc $C -d "$OUT/${V}_$C" -o run --output-format csv -- \
+    RT_ALLOW_EXPERIMENT=1 RT_MI355X_LIB=$LIB timeout -s KILL 90 rocprofv3 --pmc $C -d "$OUT/${V}_$C" -o run --output-format csv -- \
         python3 bench.py --config $CFG --precision $PREC --steps 1 --warmup 0 --cpu-seconds 0 --other-precision 0 \
         > "$OUT/${V}_$C.log" 2>&1 || { echo "$V $C failed"; exit 1; }
   done
