@@ -2,7 +2,7 @@
 //
 //   rt-render [--scene scene.toml] [--width 3840] [--height 2160] [--spp 100] [--bounces 50]
 //             [--seed 0x5EED0001] [--f32] [--root2] [--mode vectorized2|vectorized|vectorized3|scalar]
-//             [--out output.png|.ppm] [--dump-scene]
+//             [--out output.png|.ppm] [--block-size B] [--dump-scene]
 //
 // --mode picks which of the reference's renderers is reproduced (include/rt_mi355x.h): the live
 // render_vectorized2 (default), render_vectorized, or the scalar render.
@@ -66,7 +66,7 @@ static void dump_scene(const Scene& sc) {
 
 int main(int argc, char** argv) {
     std::string scene_path = "scene.toml", out = "output.png";
-    uint32_t width = 3840, height = 2160, spp = 100, bounces = 50, flags = 0;
+    uint32_t width = 3840, height = 2160, spp = 100, bounces = 50, flags = 0, block_size = 0;
     uint64_t seed = 0x5EED0001ull;
     bool dump = false;
     for (int i = 1; i < argc; ++i) {
@@ -92,10 +92,12 @@ int main(int argc, char** argv) {
             else if (m != "vectorized2") { std::fprintf(stderr, "unknown mode %s\n", m.c_str()); return 2; }
         }
         else if (a == "--out") out = next();
+        else if (a == "--block-size") block_size = (uint32_t)std::stoul(next());
         else if (a == "--dump-scene") dump = true;
         else if (a == "-h" || a == "--help") {
             std::puts("rt-render [--scene scene.toml] [--width W] [--height H] [--spp S] [--bounces B] [--seed N] "
-                      "[--f32] [--root2] [--mode vectorized2|vectorized|vectorized3|scalar] [--out output.png] [--dump-scene]");
+                      "[--f32] [--root2] [--mode vectorized2|vectorized|vectorized3|scalar] [--out output.png] [--block-size B] "
+                      "[--dump-scene]");
             return 0;
         } else { std::fprintf(stderr, "unknown argument %s\n", a.c_str()); return 2; }
     }
@@ -122,7 +124,7 @@ int main(int argc, char** argv) {
         std::printf("\tViewport Top Left Corner: %s\n", rs3(camera.c.ulc).c_str());
         std::printf("\t Number of objects: \t %zu\n", scene.len());                           // main.rs:60
 
-        GpuRenderer renderer(seed, flags);
+        GpuRenderer renderer(seed, flags, block_size);   // block_size 128: TileRenderer::new(None, 128), main.rs:62
         std::fprintf(stderr, "Rendering %u by %u image on %s (%s)...\n", width, height, rt_version(),
                      (flags & RT_FLAG_F32) ? "fp32" : "fp64");
         auto [image, stat] = renderer.render(bounces, spp, scene, camera);                     // main.rs:64

@@ -272,10 +272,16 @@ struct Renderer {   // renderer.rs:38-40
 };
 
 // The GPU implementation of Renderer (replaces TileRenderer, renderer.rs:232-387).
+// block_size 0: the whole image in one launch (rt_render).  block_size B > 0: TileRenderer's
+// decomposition (renderer.rs:248-266): B x B blocks, row-major, one launch each on one device
+// context, and after each the reference's per-block line (renderer.rs:339), with the block's pixel
+// rate from the launch's kernel time: "Device 0 complete block (x, y) at R px/s".  The image is the
+// same either way (the RNG is keyed by the global pixel index).
 struct GpuRenderer : Renderer {
     uint64_t seed;
     uint32_t flags;
-    explicit GpuRenderer(uint64_t s = 0x5EED0001ull, uint32_t f = 0) : seed(s), flags(f) {}
+    uint32_t block_size;
+    explicit GpuRenderer(uint64_t s = 0x5EED0001ull, uint32_t f = 0, uint32_t b = 0) : seed(s), flags(f), block_size(b) {}
     std::pair<RgbImage, RenderStat> render(size_t max_bounces, size_t spp, const Scene& scene,
                                            const Camera& camera) override {
         const auto t0 = std::chrono::steady_clock::now();
@@ -284,13 +290,63 @@ struct GpuRenderer : Renderer {
         RgbImage img{camera.image_width(), camera.image_height(), {}};
         img.data.resize((size_t)img.width * img.height * 3);
         rt_stats st{};
-        const int rc = rt_render(&rs, &camera.c, (uint32_t)max_bounces, (uint32_t)spp, seed, flags, nullptr,
-                                 img.data.data(), nullptr, &st);
-        if (rc == RT_ERR_RANGE) throw Panic(std::string("assertion failed: ") + rt_last_error());
-        if (rc != RT_OK) throw Panic(std::string("rt_render failed: ") + rt_last_error());
+        if (block_size == 0) {
+            const int rc = rt_render(&rs, &camera.c, (uint32_t)max_bounces, (uint32_t)spp, seed, flags, nullptr,
+                                     img.data.data(), nullptr, &st);
+            if (rc == RT_ERR_RANGE) throw Panic(std::string("assertion failed: ") + rt_last_error());
+            if (rc != RT_OK) throw Panic(std::string("rt_render failed: ") + rt_last_error());
+        } else {
+            render_blocks(rs, camera, (uint32_t)max_bounces, (uint32_t)spp, img, st);
+        }
         const size_t npx = (size_t)img.width * img.height;
         RenderStat stat(std::chrono::steady_clock::now() - t0, npx, st);
         return {std::move(img), stat};
+    }
+
+  private:
+    void render_blocks(const rt_scene& rs, const Camera& camera, uint32_t max_bounces, uint32_t spp, RgbImage& img,
+                       rt_stats& total) {
+        struct Ctx {
+            rt_context* c = nullptr;
+            void* buf = nullptr;
+            ~Ctx() { if (buf) rt_device_free(c, buf); if (c) rt_context_destroy(c); }
+        } x;
+        auto chk = [](int rc, const char* what) {
+            if (rc == RT_ERR_RANGE) throw Panic(std::string("assertion failed: ") + rt_last_error());
+            if (rc != RT_OK) throw Panic(std::string(what) + ": " + rt_last_error());
+        };
+        chk(rt_context_create(0, &x.c), "rt_context_create");
+        chk(rt_context_set_scene(x.c, &rs), "rt_context_set_scene");
+        const uint32_t B = block_size, W = img.width, H = img.height;
+        chk(rt_device_alloc(x.c, (size_t)B * B * 3, &x.buf), "rt_device_alloc");
+        std::vector<uint8_t> tile((size_t)B * B * 3);
+        const uint32_t nbx = (W + B - 1) / B, nby = (H + B - 1) / B;   // renderer.rs:248-266
+        bool range_err = false;
+        for (uint32_t by = 0; by < nby; ++by)
+            for (uint32_t bx = 0; bx < nbx; ++bx) {
+                const uint32_t c0 = bx * B, r0 = by * B;
+                const rt_tile_range tr{r0, 1, std::min(B, H - r0), c0, std::min(B, W - c0)};
+                chk(rt_render_async(x.c, &camera.c, max_bounces, spp, seed, flags, &tr, x.buf, nullptr, nullptr),
+                    "rt_render_async");
+                rt_stats st{};
+                const int rc = rt_context_collect(x.c, nullptr, &st);
+                if (rc == RT_ERR_RANGE) range_err = true;
+                else chk(rc, "rt_context_collect");
+                const size_t npx = (size_t)tr.row_count * tr.col_count;
+                chk(rt_memcpy_d2h(x.c, tile.data(), x.buf, npx * 3), "rt_memcpy_d2h");
+                for (uint32_t r = 0; r < tr.row_count; ++r)
+                    std::memcpy(&img.data[((size_t)(r0 + r) * W + c0) * 3], &tile[(size_t)r * tr.col_count * 3],
+                                (size_t)tr.col_count * 3);
+                // renderer.rs:339: "Thread {} complete block ({}, {}) at {:.2} px/s"
+                std::printf("Device 0 complete block (%u, %u) at %.2f px/s\n", bx, by, st.pixels_per_second);
+                total.kernel_ms += st.kernel_ms;
+                total.pixels += st.pixels;
+                total.samples += st.samples;
+                total.ray_segments += st.ray_segments;
+                total.lane_slots += st.lane_slots;
+                total.bounce_iters += st.bounce_iters;
+            }
+        if (range_err) throw Panic("assertion failed: a pixel channel exceeded 2.0 (color.rs:55-57)");
     }
 };
 

@@ -314,6 +314,25 @@ def test_cli_renders_config_a_from_toml(tmp_path):
         np.testing.assert_array_equal(img, want)
 
 
+def test_cli_block_size_prints_per_block_rates(tmp_path):
+    """rt-render --block-size 128: TileRenderer's 128x128 blocks (renderer.rs:248-266), one launch each,
+    one "complete block (x, y) at R px/s" line per block (renderer.rs:339); the same image."""
+    import re
+    import subprocess
+    cli = os.path.join(os.path.dirname(GOLDEN), "..", "rust-ray-tracing_amd", "bin", "rt-render")
+    (tmp_path / "scene.toml").write_text(rt.scenes.scene_to_toml(rt.scenes.three_spheres()))
+    want = np.load(os.path.join(GOLDEN, "config_a.npz"))["rgb8"]
+    r = subprocess.run([cli, "--width", "400", "--height", "225", "--spp", "16", "--bounces", "8", "--out", "o.ppm",
+                        "--block-size", "128"], cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    blocks = re.findall(r"^Device 0 complete block \((\d+), (\d+)\) at ([0-9.]+) px/s$", r.stdout, flags=re.M)
+    assert sorted((int(x), int(y)) for x, y, _ in blocks) == [(x, y) for x in range(4) for y in range(2)]
+    assert all(float(v) > 0 for _, _, v in blocks)
+    raw = (tmp_path / "o.ppm").read_bytes()
+    assert raw.startswith(b"P6")
+    np.testing.assert_array_equal(np.frombuffer(raw[-400 * 225 * 3:], np.uint8).reshape(225, 400, 3), want)
+
+
 @pytest.mark.parametrize("flags,spp", [(abi.RT_FLAG_F32, 2048), (0, 256)])
 def test_config_e_scene(renderer, flags, spp):
     """Config E's 10 000-sphere scene (2 500 scalar-load groups per ray) at config E's spp (fp32)."""

@@ -21,10 +21,10 @@ print("nccl world-1 identical:", np.array_equal(a, b), " gloo world-2 identical:
       " self-launched world-2 identical:", np.array_equal(a, d), a.shape)
 for n in ("single", "nccl1", "gloo2", "self2"):   # the decomposition rank 0 prints (bench.py "dist")
     line = json.loads([l for l in open(f"{o}/{n}.log") if l.startswith("{")][-1])
-    d = line["dist"]
-    print(n, "value", line["value"], "n_gpus", line["n_gpus"], "backend", d["backend"], "world_size_initialised",
-          d["world_size_initialised"], "rccl", d["rccl_version"], "imbalance", d.get("imbalance"))
-    for r in d["per_rank"]:
+    dd = line["dist"]
+    print(n, "value", line["value"], "n_gpus", line["n_gpus"], "backend", dd["backend"], "world_size_initialised",
+          dd["world_size_initialised"], "rccl", dd["rccl_version"], "imbalance", dd.get("imbalance"))
+    for r in dd["per_rank"]:
         print("   rank", r["rank"], "render_ms", r["render_ms"], "gather_ms", r["gather_ms"], "assemble_ms",
               r["assemble_ms"], "wall_s", r["wall_s"], "px_per_s", r["px_per_s"])
 assert np.array_equal(a, b) and np.array_equal(a, c) and np.array_equal(a, d)
