@@ -59,7 +59,8 @@
                             defined(RT_EXP_BLOCK_SAMPLES) || defined(RT_EXP_TMUL) || defined(RT_EXP_OLD_REPLAY) ||   \
                             defined(RT_EXP_NO_PARK) || defined(RT_EXP_PARKC_ALL) || defined(RT_EXP_DUP_FINISH) ||    \
                             defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
-                            defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_KSTATS))
+                            defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
+                            defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
 #ifndef RT_SRC_HASH
@@ -1078,6 +1079,115 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+// The cone cull over the sweep layout (whole wave, wave-uniform control flow): calls pass(sl) for every
+// sphere slot whose cone-cull record {w = c - O, rp} the cone with axis a, sin S and cos Cc does not
+// cull (all: every record passes).  Returns the wave-level cone tests run.  xw0, kw0: the first
+// records of both levels, loaded by the caller before the cone's setup.
+template <bool MEGA, typename KP, typename F>
+__device__ __forceinline__ uint32_t cone_walk(const KP& q, float ax, float ay, float az, float S, float Cc, bool all,
+                                              const float4& xw0, const float4& kw0, F&& pass) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const float4* cs = (const float4*)__builtin_assume_aligned(q.cull, 16);    // per slot (sweep layout)
+    const float4* cc = (const float4*)__builtin_assume_aligned(q.cullc, 16);   // per cluster
+    const uint32_t nx = 4u * q.n_xg, ncl = 4u * q.n_top;
+    // cone test of a record {w = c - O, rp}; padding records (rp = -inf) never pass
+    auto cone = [&](const float4& wc) -> bool {
+        const float t = __builtin_fmaf(wc.z, az, __builtin_fmaf(wc.y, ay, wc.x * ax));
+        const float px = __builtin_fmaf(wc.y, az, -(wc.z * ay)), py = __builtin_fmaf(wc.z, ax, -(wc.x * az)),
+                    pz = __builtin_fmaf(wc.x, ay, -(wc.y * ax));
+        const float pp = __builtin_amdgcn_sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
+        const float f = __builtin_fmaf(pp, Cc, -(t * S));
+        return wc.w > -INFINITY && (all || !(f > wc.w));   // NaN f passes
+    };
+    uint32_t n_cone = 0;
+    // 1. the always-exact spheres (build_layout's leading slots), lanes as spheres
+    for (uint32_t base = 0; base < nx; base += 64u) {
+        ++n_cone;
+        unsigned long long m = __ballot(base + lane < nx && cone(base == 0 ? xw0 : cs[base + lane]));
+        while (m != 0ull) {
+            const uint32_t sl = base + (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            pass(sl);
+        }
+    }
+    // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
+    // to 4 passing clusters per pass, 16 lanes each.  M: ballot of a cluster test in which lane L
+    // tested cluster klane(L).
+    auto members = [&](unsigned long long M, uint32_t klane) {
+        while (M != 0ull) {
+            ++n_cone;
+            uint32_t k[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // empty quarters take the padding cluster ncl (all dummies)
+                k[j] = M != 0ull ? (uint32_t)__builtin_amdgcn_readlane(klane, (int)__builtin_ctzll(M)) : ncl;
+                M &= M - 1ull;
+            }
+            const uint32_t qd = lane >> 4;
+            const uint32_t kl = qd == 0 ? k[0] : qd == 1 ? k[1] : qd == 2 ? k[2] : k[3];
+            unsigned long long m = __ballot(cone(cs[nx + 16u * kl + (lane & 15u)]));
+            while (m != 0ull) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                const uint32_t kb = (b >> 4) == 0 ? k[0] : (b >> 4) == 1 ? k[1] : (b >> 4) == 2 ? k[2] : k[3];
+                pass(nx + 16u * kb + (b & 15u));
+            }
+        }
+    };
+    const uint32_t nsu = MEGA ? q.n_supc : 0u;   // the super level exists only in the MEGA kernels
+    if (nsu == 0u) {
+        for (uint32_t cb = 0; cb < ncl; cb += 64u) {
+            ++n_cone;
+            members(__ballot(cone(cb == 0 ? kw0 : cc[cb + lane])), cb + lane);   // padded to whole 64s
+        }
+    } else {
+        // big scenes: lanes as supers first (their records, after the clusters', bound every member
+        // sphere's record the same way), then the 4 clusters of up to 16 passing supers per pass
+        const float4* csu = cc + q.n_clp;
+        for (uint32_t sb = 0; sb < nsu; sb += 64u) {
+            ++n_cone;
+            unsigned long long SM = __ballot(cone(csu[sb + lane]));   // padded to whole 64s (rp = -inf)
+            while (SM != 0ull) {
+                uint32_t mys = 0xFFFFFFFFu;
+                for (uint32_t j = 0; j < 16u && SM != 0ull; ++j) {
+                    const uint32_t sj = sb + (uint32_t)__builtin_ctzll(SM);
+                    SM &= SM - 1ull;
+                    if ((lane >> 2) == j) mys = sj;
+                }
+                const bool have = mys != 0xFFFFFFFFu;
+                const uint32_t kl = have ? 4u * mys + (lane & 3u) : ncl;
+                ++n_cone;
+                members(__ballot(have && cone(cc[kl])), kl);
+            }
+        }
+    }
+    return n_cone;
+}
+
+// The reference's exact test (objects.rs:252-257 on the camera-origin table) of sphere slot sl for the
+// camera rays of lanes v; the scene index (hit_update's tie rule and the result) comes with it.
+template <typename T, bool root2, bool SCALAR, typename KP>
+__device__ __forceinline__ void camera_exact(const KP& q, uint32_t sl, bool v, const V3<T>& d, T a, T inv_a, T& best_t,
+                                             int& best) {
+    KSTAT(2);
+    constexpr bool kBothRoots = root2 || SCALAR;
+    cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
+    cptr<uint32_t> ri = (cptr<uint32_t>)q.ridx;
+    const uint32_t i = ri[sl];
+    const T ocx = cxt[4 * sl], ocy = cxt[4 * sl + 1], ocz = cxt[4 * sl + 2], c = cxt[4 * sl + 3];
+    if (v) {
+        T hb, disc;
+        if constexpr (SCALAR) {   // objects.rs:217-222
+            hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
+            disc = hb * hb - a * c;
+        } else {                  // objects.rs:255, 257
+            hb = fma(ocz, d.z, fma(ocy, d.y, ocx * d.x));
+            disc = fma(hb, hb, (-a) * c);
+        }
+        if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
+            hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
+    }
+}
+
 template <typename T, bool root2, bool SCALAR, bool MEGA = false>
 __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1115,106 +1225,111 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const float S = ufl(__builtin_fmaf(__builtin_amdgcn_sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f));
     if (!(S < 0.5f)) all = true;
     const float Cc = ufl(__builtin_amdgcn_sqrtf(__builtin_fmaf(-S, S, 1.0f)));
-    cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
-    cptr<uint32_t> ri = (cptr<uint32_t>)q.ridx;
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
     T best_t = T(INFINITY);
     int best = -1;
-    constexpr bool kBothRoots = root2 || SCALAR;
     KSTAT(3);
-    // cone test of a record {w = c - O, rp}; padding records (rp = -inf) never pass
-    auto cone = [&](const float4& wc) -> bool {
-        const float t = __builtin_fmaf(wc.z, az, __builtin_fmaf(wc.y, ay, wc.x * ax));
-        const float px = __builtin_fmaf(wc.y, az, -(wc.z * ay)), py = __builtin_fmaf(wc.z, ax, -(wc.x * az)),
-                    pz = __builtin_fmaf(wc.x, ay, -(wc.y * ax));
-        const float pp = __builtin_amdgcn_sqrtf(__builtin_fmaf(pz, pz, __builtin_fmaf(py, py, px * px)));
-        const float f = __builtin_fmaf(pp, Cc, -(t * S));
-        return wc.w > -INFINITY && (all || !(f > wc.w));   // NaN f passes
-    };
-    // the reference's exact test (objects.rs:252-257 on the camera-origin table) for slot sl; the
-    // scene index (for hit_update's tie rule and the result) comes with it, one round trip
-    auto exact = [&](uint32_t sl) {
-        KSTAT(2);
-        const uint32_t i = ri[sl];
-        const T ocx = cxt[4 * sl], ocy = cxt[4 * sl + 1], ocz = cxt[4 * sl + 2], c = cxt[4 * sl + 3];
-        if (v) {
-            T hb, disc;
-            if constexpr (SCALAR) {   // objects.rs:217-222
-                hb = (ocx * d.x + ocy * d.y) + ocz * d.z;
-                disc = hb * hb - a * c;
-            } else {                  // objects.rs:255, 257
-                hb = fma(ocz, d.z, fma(ocy, d.y, ocx * d.x));
-                disc = fma(hb, hb, (-a) * c);
-            }
-            if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
-                hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
-        }
-    };
-    uint32_t n_cone = 0, n_cx = 0;   // executed-work counts (work_add below)
-    // 1. the always-exact spheres (build_layout's leading slots), lanes as spheres
-    for (uint32_t base = 0; base < nx; base += 64u) {
-        ++n_cone;
-        unsigned long long m = __ballot(base + lane < nx && cone(base == 0 ? xw0 : cs[base + lane]));
-        n_cx += (uint32_t)__popcll(m);
-        while (m != 0ull) {
-            const uint32_t s = base + (uint32_t)__builtin_ctzll(m);
-            m &= m - 1ull;
-            exact(s);
-        }
-    }
-    // 2. clusters: lanes as clusters (records bound every member's record), then the members of up
-    // to 4 passing clusters per pass, 16 lanes each.  M: ballot of a cluster test in which lane L
-    // tested cluster klane(L).
-    auto members = [&](unsigned long long M, uint32_t klane) {
-        while (M != 0ull) {
-            ++n_cone;
-            uint32_t k[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {   // empty quarters take the padding cluster ncl (all dummies)
-                k[j] = M != 0ull ? (uint32_t)__builtin_amdgcn_readlane(klane, (int)__builtin_ctzll(M)) : ncl;
-                M &= M - 1ull;
-            }
-            const uint32_t qd = lane >> 4;
-            const uint32_t kl = qd == 0 ? k[0] : qd == 1 ? k[1] : qd == 2 ? k[2] : k[3];
-            unsigned long long m = __ballot(cone(cs[nx + 16u * kl + (lane & 15u)]));
-            n_cx += (uint32_t)__popcll(m);
-            while (m != 0ull) {
-                const uint32_t b = (uint32_t)__builtin_ctzll(m);
-                m &= m - 1ull;
-                const uint32_t kb = (b >> 4) == 0 ? k[0] : (b >> 4) == 1 ? k[1] : (b >> 4) == 2 ? k[2] : k[3];
-                exact(nx + 16u * kb + (b & 15u));
-            }
-        }
-    };
-    const uint32_t nsu = MEGA ? q.n_supc : 0u;   // the super level exists only in the MEGA kernels
-    if (nsu == 0u) {
-        for (uint32_t cb = 0; cb < ncl; cb += 64u) {
-            ++n_cone;
-            members(__ballot(cone(cb == 0 ? kw0 : cc[cb + lane])), cb + lane);   // padded to whole 64s
-        }
-    } else {
-        // big scenes: lanes as supers first (their records, after the clusters', bound every member
-        // sphere's record the same way), then the 4 clusters of up to 16 passing supers per pass
-        const float4* csu = cc + q.n_clp;
-        for (uint32_t sb = 0; sb < nsu; sb += 64u) {
-            ++n_cone;
-            unsigned long long S = __ballot(cone(csu[sb + lane]));   // padded to whole 64s (rp = -inf)
-            while (S != 0ull) {
-                uint32_t mys = 0xFFFFFFFFu;
-                for (uint32_t j = 0; j < 16u && S != 0ull; ++j) {
-                    const uint32_t sj = sb + (uint32_t)__builtin_ctzll(S);
-                    S &= S - 1ull;
-                    if ((lane >> 2) == j) mys = sj;
-                }
-                const bool have = mys != 0xFFFFFFFFu;
-                const uint32_t kl = have ? 4u * mys + (lane & 3u) : ncl;
-                ++n_cone;
-                members(__ballot(have && cone(cc[kl])), kl);
-            }
-        }
-    }
+    uint32_t n_cx = 0;   // executed-work counts (work_add below)
+    const uint32_t n_cone = cone_walk<MEGA>(q, ax, ay, az, S, Cc, all, xw0, kw0, [&](uint32_t sl) {
+        ++n_cx;
+        camera_exact<T, root2, SCALAR>(q, sl, v, d, a, inv_a, best_t, best);
+    });
     work_add(kWCone, n_cone);
+    work_add(kWCExact, n_cx);
+    t_out = best_t;
+    return best;
+}
+
+// Per-pixel camera candidate lists (camera batches): every primary ray of pixel (col, row) starts at
+// the camera centre O and points into the pixel's footprint, the parallelogram ulc + vu (col + x) / W
+// + vv (row + y) / H, x, y in [0, 1] (ray_tracing.rs:80-84).  Its directions form a convex set whose
+// largest angle from the axis (the direction to the footprint's centre) is taken at a corner, so the
+// cone with that axis and sin S = max over the 4 corners of |D x a| / |D| (fp32, inflated like the
+// batch cone: 4 u relative + 8 u) contains every exactly computed ray.  The pixel margin 2^-20 M / |Dc|
+// (M = |ulc|_1 + |vu|_1 + |vv|_1 + |centre|_1, Dc the centre's direction) covers the rounding of the
+// corners here and of the rays themselves in T, which grows with the coordinates' magnitudes over the
+// focal distance (tests/pixel_cone_fuzz.c: every computed ray inside, worst case 7 % of the margin).
+// The cone walk runs ONCE per pixel, when its slot opens, and records the passing sphere slots (at most
+// kCList - 1; more, a cone over 60 degrees, or a slot index past u16: list[0] = 0xFFFF, and the
+// pixel's batches run the per-batch camera_sweep instead).  A batch then runs the exact test of the
+// listed spheres of its pixels only: for a lane, the union of its batch's lists holds every sphere its
+// ray can hit, and extra exact tests never change a result.
+constexpr uint32_t kCList = 8;
+template <typename T, bool MEGA>
+__device__ __forceinline__ uint32_t pixel_list(uint32_t col, uint32_t row, uint16_t* list) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const auto& q = *cold_args<T>();
+    const float4* cs = (const float4*)__builtin_assume_aligned(q.cull, 16);
+    const float4* cc = (const float4*)__builtin_assume_aligned(q.cullc, 16);
+    const uint32_t nx = 4u * q.n_xg, ncl = 4u * q.n_top;
+    const float4 kPad = {0.0f, 0.0f, 0.0f, -INFINITY};
+    const float4 xw0 = lane < nx ? cs[lane] : kPad, kw0 = lane < ncl ? cc[lane] : kPad;
+    // lanes 0..3: the footprint's corners, lane 4 its centre (fp32)
+    const float fx = lane < 4u ? (float)(lane & 1u) : 0.5f, fy = lane < 4u ? (float)(lane >> 1) : 0.5f;
+    const float s1 = ((float)col + fx) / (float)q.W, s2 = ((float)row + fy) / (float)q.H;
+    const float Dx = ((float)q.ulc[0] + ((float)q.vu[0] * s1 + (float)q.vv[0] * s2)) - (float)q.center[0];
+    const float Dy = ((float)q.ulc[1] + ((float)q.vu[1] * s1 + (float)q.vv[1] * s2)) - (float)q.center[1];
+    const float Dz = ((float)q.ulc[2] + ((float)q.vu[2] * s1 + (float)q.vv[2] * s2)) - (float)q.center[2];
+    float ax = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(Dx), 4));
+    float ay = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(Dy), 4));
+    float az = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(Dz), 4));
+    const float ia = __builtin_amdgcn_rsqf(__builtin_fmaf(az, az, __builtin_fmaf(ay, ay, ax * ax)));
+    ax = ufl(ax * ia);
+    ay = ufl(ay * ia);
+    az = ufl(az * ia);
+    const float cx = __builtin_fmaf(Dy, az, -(Dz * ay)), cy = __builtin_fmaf(Dz, ax, -(Dx * az)),
+                cz = __builtin_fmaf(Dx, ay, -(Dy * ax));
+    const float dn2 = __builtin_fmaf(Dz, Dz, __builtin_fmaf(Dy, Dy, Dx * Dx));
+    const bool corner = lane < 4u;
+    const float s2c = corner ? __builtin_fmaf(cz, cz, __builtin_fmaf(cy, cy, cx * cx)) * __builtin_amdgcn_rcpf(dn2) * (1.0f + 0x1.0p-22f) : 0.0f;
+    const float dt = (__builtin_fmaf(Dz, az, __builtin_fmaf(Dy, ay, Dx * ax))) * __builtin_amdgcn_rsqf(dn2);
+    bool over = __ballot(corner && !(dt > 0.5f)) != 0ull;   // a corner > 60 deg off the axis (or NaN)
+    const uint32_t sm = wave_max_dpp(__float_as_uint(s2c));
+    float M = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        M += ((fabsf((float)q.ulc[k]) + fabsf((float)q.vu[k])) + fabsf((float)q.vv[k])) + fabsf((float)q.center[k]);
+    const float dnc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(dn2), 4));
+    const float margin = (M * 0x1.0p-20f) * __builtin_amdgcn_rsqf(dnc);
+    const float S = ufl(__builtin_fmaf(__builtin_amdgcn_sqrtf(__uint_as_float(sm)), 1.0f + 0x1.0p-22f, 0x1.0p-21f + margin));
+    if (!(S < 0.5f)) over = true;
+    const float Cc = ufl(__builtin_amdgcn_sqrtf(__builtin_fmaf(-S, S, 1.0f)));
+    uint32_t n = 0;
+    uint32_t n_cone = 0;
+    if (!over) {
+        n_cone = cone_walk<MEGA>(q, ax, ay, az, S, Cc, false, xw0, kw0, [&](uint32_t sl) {
+            if (sl >= 0xFFFFu) over = true;
+            else if (n + 1u < kCList && lane == 0) list[1u + n] = (uint16_t)sl;
+            ++n;
+        });
+    }
+    if (over || n + 1u > kCList) n = 0xFFFFu;
+    if (lane == 0) list[0] = (uint16_t)n;
+    work_add(kWCone, n_cone);
+    return n;
+}
+
+// A camera batch against its pixels' candidate lists (slots in smask): the exact test of every listed
+// sphere for every lane (a lane of one pixel also tests the other pixel's spheres: extra exact tests
+// never change a result).
+template <typename T, bool root2, bool SCALAR>
+__device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, const uint16_t (*lists)[kCList],
+                                             uint32_t smask) {
+    const auto& q = *cold_args<T>();
+    const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
+    const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
+    T best_t = T(INFINITY);
+    int best = -1;
+    uint32_t n_cx = 0;
+    for (; smask != 0u; smask &= smask - 1u) {
+        const uint16_t* l = lists[__builtin_ctz(smask)];
+        const uint32_t n = __builtin_amdgcn_readfirstlane(l[0]);
+        for (uint32_t j = 0; j < n; ++j) {
+            ++n_cx;
+            camera_exact<T, root2, SCALAR>(q, __builtin_amdgcn_readfirstlane(l[1u + j]), v, d, a, inv_a, best_t, best);
+        }
+    }
     work_add(kWCExact, n_cx);
     t_out = best_t;
     return best;
@@ -1489,7 +1604,8 @@ template <typename T> __device__ __forceinline__ PScratch<T> wave_scratch(uint32
 }
 
 // Wave-uniform issue state, parked in LDS between refills for the same reason.
-struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, drained, qhead, qcount, blk_next, blk_end; };
+// need: slots opened since their pixel's camera candidate list was last built (camera batches)
+struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, drained, qhead, qcount, blk_next, blk_end, need; };
 
 // Work items (pixels) are claimed in blocks.  One global counter counts blocks, and block j's items
 // are a fixed function of j (guided_block): sizes G, G/2, ..., 2 while more than G T, ..., 2T items
@@ -1554,19 +1670,33 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
+// The position map in LDS (live-path kernels without the mega level, P <= kLMapCap positions: config C's
+// 512 spp): the replay's scattered u16 writes, the map's initialisation and the reduction's reads stay
+// on the CU instead of going to HBM as partial lines.  Larger P uses the global map in PScratch.
+#ifndef RT_EXP_LMAP_CAP
+#define RT_EXP_LMAP_CAP 512
+#endif
+constexpr uint32_t kLMapCap = RT_EXP_LMAP_CAP;
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
-                                                 T (*stage)[64]) {
+                                                 T (*stage)[64], uint16_t* lmap) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
     constexpr uint32_t kNone = PScratch<T>::kNone;
+    const bool lm = kLMapCap > 0u && lmap != nullptr && P <= kLMapCap;   // wave-uniform
+    auto set_map = [&](uint32_t qq, uint32_t smp) {
+        if (lm) lmap[qq] = (uint16_t)smp;
+        else sc.set_map(qq, smp);
+    };
     // Map init: no position holds a terminated sample's value yet (survivors and never-written
     // positions read 0; positions [spp, P), the missing lanes of a partial last chunk, get their
     // fixed value in the final reduction).  Two u16 entries per u32 store.
     if (MODE == kModeV2) {
-        if (sc.wide & 2u) {
+        if (lm) {
+            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(lmap + qi) = 0xFFFFFFFFu;
+        } else if (sc.wide & 2u) {
             for (uint32_t qi = lane; qi < P; qi += 64u) sc.set_map(qi, kNone);
         } else {
             for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(sc.base + 2u * qi) = 0xFFFFFFFFu;
@@ -1659,8 +1789,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                     const bool U = q.s_sel == (ek & 1u);
                     const bool w_old = U && pold >= lo && pold < hi;
                     const bool w_new = !U || pnew < lo || pnew >= hi;
-                    if (w_old || w_new) sc.set_map(w_old ? pold : pnew, i);
-                    if (w_old && w_new) sc.set_map(pnew, i);
+                    if (w_old || w_new) set_map(w_old ? pold : pnew, i);
+                    if (w_old && w_new) set_map(pnew, i);
                 }
             }
         }
@@ -1760,8 +1890,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                     const bool w_old = U && pold >= lo && pold < hi;
                     const bool w_new = !U || pnew < lo || pnew >= hi;
                     // At most one position except when the old one retires now and the new one later.
-                    if (w_old || w_new) sc.set_map(w_old ? pold : pnew, i);
-                    if (w_old && w_new) sc.set_map(pnew, i);
+                    if (w_old || w_new) set_map(w_old ? pold : pnew, i);
+                    if (w_old && w_new) set_map(pnew, i);
                 }
                 cge += (uint32_t)__popcll(bge);
                 ceq += (uint32_t)__popcll(beq);
@@ -1827,7 +1957,13 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                         else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
                     }
                 } else if constexpr (MODE == kModeV2) {
-                    const uint32_t m = sc.map(qq);
+                    uint32_t m;
+                    if (lm) {
+                        m = lmap[qq];
+                        if (m == 0xFFFFu) m = kNone;
+                    } else {
+                        m = sc.map(qq);
+                    }
                     if (m != kNone) {
                         const C3<T> cm = sc.c(s, m);
                         const V3<T> sk = sky(sc.y(s, qq));
@@ -1891,7 +2027,10 @@ constexpr uint32_t kQCap = 128;   // camera-batch queue entries per wave (a batc
 template <typename T, int W, bool ROOT2, int MODE = kModeV2, bool CAMQ = false, bool MEGA = false>
 __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     constexpr bool SC = MODE == kModeScalar;
-    constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? kQCap : 1;
+    // fp64 at 5+ waves per SIMD: a 64-entry queue (half the LDS), so the parked ray fits in 32 KB per
+    // workgroup
+    constexpr bool kF64Park = sizeof(T) == 8 && W >= 5;
+    constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? (kF64Park ? 64u : kQCap) : 1;
     __shared__ unsigned long long wcount[4][3];
     // 8-byte aligned: finish_pixel keeps its 12 running sums (T, fp64 too) in this array
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[4][64];
@@ -1902,13 +2041,15 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ uint32_t s_slotpix[4][kSlots];   // the pixel of each open slot
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
+    // camera candidate list of each open pixel slot (pixel_list): [0] = count (0xFFFF: none, sweep per batch)
+    __shared__ uint16_t s_clist[QW][CAMQ ? kSlots : 1][kCList];
     // fp32 at 6 waves per SIMD (80 VGPRs): each lane's ray origin and direction are parked in LDS
     // across the sphere sweeps and the camera batches and re-read right before the scatter, instead
     // of being held in VGPRs (the allocator otherwise spills them to scratch memory around the sweep).
 #ifdef RT_EXP_NO_PARK
     constexpr bool kPark = false;
 #else
-    constexpr bool kPark = sizeof(T) == 4 && W >= 6;
+    constexpr bool kPark = (sizeof(T) == 4 && W >= 6) || kF64Park;
 #endif
     // the mega-level kernels park the path colour as well (their four-level sweep holds more state)
 #ifdef RT_EXP_PARKC_ALL
@@ -1917,6 +2058,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     constexpr bool kParkC = kPark && MEGA;
 #endif
     __shared__ T s_park[kPark ? 4 : 1][kParkC ? 9 : 6][64];
+    // finish_pixel's position map (P <= kLMapCap) in LDS: the fp64 live-path kernels without the mega level
+    // (fp64 C +1.1 % same-box).  fp32 lost 7 % with it (the extra finish_pixel code pushed 5 more spills
+    // into the hot loop at 80 VGPRs); the mega kernels' LDS is full at 6 waves per SIMD.
+    constexpr bool kLMap = MODE == kModeV2 && !MEGA && kLMapCap > 0u && sizeof(T) == 8 && !kF64Park;
+    __shared__ __attribute__((aligned(16))) uint16_t s_lmap[kLMap ? 4 : 1][kLMap ? kLMapCap : 2];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
@@ -1925,7 +2071,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     if (threadIdx.x == 0) s_pool = 0ull;   // {next, end} = {0, 0}: empty
     __syncthreads();
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
@@ -1970,6 +2116,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         bool drained = __builtin_amdgcn_readfirstlane(s_is[wave].drained) != 0u;
         uint32_t blk_next = __builtin_amdgcn_readfirstlane(s_is[wave].blk_next);
         uint32_t blk_end = __builtin_amdgcn_readfirstlane(s_is[wave].blk_end);
+        uint32_t opened = 0;
         while (want != 0ull && !drained) {
             if (cur_next == spp) {
                 const uint32_t avail = ~busy & ((1u << kSlots) - 1u);
@@ -2015,6 +2162,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 if (lane == s) { slot_item = item; slot_left = spp; }
                 if (lane == 0) s_slotpix[wave][s] = cur_pix;
                 busy |= 1u << s;
+                opened |= 1u << s;
                 cur = s;
                 cur_next = 0;
             }
@@ -2030,6 +2178,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             s_is[wave].busy = busy; s_is[wave].cur = cur; s_is[wave].cur_next = cur_next; s_is[wave].cur_pix = cur_pix;
             s_is[wave].cur_row = cur_row; s_is[wave].cur_col = cur_col; s_is[wave].drained = drained ? 1u : 0u;
             s_is[wave].blk_next = blk_next; s_is[wave].blk_end = blk_end;
+            if (CAMQ) s_is[wave].need |= opened;
         }
         return got;
     };
@@ -2065,11 +2214,11 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 KSTAT(6);
 #ifdef RT_EXP_DUP_FINISH   // timing experiment: finish_pixel twice (idempotent)
                 (void)finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave],
-                                            s_stage[wave]);
+                                            s_stage[wave], kLMap ? s_lmap[wave] : nullptr);
                 wave_mem_sync();
 #endif
                 const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
-                                                         s_hist[wave], s_stage[wave]);
+                                                         s_hist[wave], s_stage[wave], kLMap ? s_lmap[wave] : nullptr);
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
@@ -2126,7 +2275,33 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             asm volatile("" ::"v"(bi2), "v"(bt2));
         }
 #endif
-        bi = camera_sweep<T, ROOT2, SC, MEGA>(v, bd, bt);   // whole wave: lanes are spheres in the cull
+        {
+            // the batch's pixel slots (one, or two where a pixel's samples end inside the batch)
+            uint32_t smask = 0;
+            for (unsigned long long m = vm; m != 0ull;) {
+                const uint32_t sl = __builtin_amdgcn_readlane(bslot, (int)__builtin_ctzll(m));
+                smask |= 1u << sl;
+                m &= ~__ballot(v && bslot == sl);
+            }
+            // each newly opened pixel's candidate list (one cone walk per pixel, not per batch)
+            uint32_t need = __builtin_amdgcn_readfirstlane(s_is[wave].need) & smask;
+            if (need != 0u) {
+                if (lane == 0) s_is[wave].need = s_is[wave].need & ~need;
+                const uint32_t iw = cold_args<T>()->W;
+                while (need != 0u) {
+                    const uint32_t sl = (uint32_t)__builtin_ctz(need);
+                    need &= need - 1u;
+                    const uint32_t pxi = __builtin_amdgcn_readfirstlane(s_slotpix[wave][sl]);
+                    const uint32_t row = pxi / iw;
+                    (void)pixel_list<T, MEGA>(pxi - row * iw, row, s_clist[wave][sl]);
+                }
+            }
+            bool listed = true;
+            for (uint32_t m = smask; m != 0u; m &= m - 1u)
+                if (__builtin_amdgcn_readfirstlane(s_clist[wave][__builtin_ctz(m)][0]) == 0xFFFFu) listed = false;
+            if (listed) bi = camera_listed<T, ROOT2, SC>(v, bd, bt, s_clist[wave], smask);
+            else bi = camera_sweep<T, ROOT2, SC, MEGA>(v, bd, bt);   // whole wave: lanes are spheres in the cull
+        }
 #else
         if (v) bi = nearest_hit<T, ROOT2, SC, true>(p, bd, bd, bt);
 #endif
@@ -2139,7 +2314,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
         const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
         if (push) {
-            const uint32_t e = (qhead + qcount + (uint32_t)__popcll(pm & lt_mask)) % kQCap;
+            const uint32_t e = (qhead + qcount + (uint32_t)__popcll(pm & lt_mask)) % QN;
             q_sid[wave][e] = bsid | (bslot << 29);
             q_hit[wave][e] = bi;
             q_t[wave][e] = bt;
@@ -2159,7 +2334,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t nfree = (uint32_t)__popcll(freem);
             for (;;) {
                 const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
-                if (qcount >= nfree || qcount + 64u > kQCap) break;
+                if (qcount >= nfree || qcount + 64u > QN) break;
                 if (!camera_batch()) break;
             }
             const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
@@ -2167,7 +2342,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t take = min(nfree, qcount);
             const uint32_t r = (uint32_t)__popcll(freem & lt_mask);
             if (!live && r < take) {
-                const uint32_t e = (qhead + r) % kQCap;
+                const uint32_t e = (qhead + r) % QN;
                 const uint32_t w0 = q_sid[wave][e];
                 sid = w0 & 0x1FFFFFFFu;
                 slot = w0 >> 29;
@@ -2185,7 +2360,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 live = true;
                 scat = true;
             }
-            if (lane == 0) { s_is[wave].qhead = (qhead + take) % kQCap; s_is[wave].qcount = qcount - take; }
+            if (lane == 0) { s_is[wave].qhead = (qhead + take) % QN; s_is[wave].qcount = qcount - take; }
         } else {
             // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
             uint32_t nsid = 0, nslot = 0, npix = 0;

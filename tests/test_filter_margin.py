@@ -115,6 +115,39 @@ def test_camera_cone_cull_is_conservative(cone_fuzz_bin, f64):
 
 
 @pytest.fixture(scope="module")
+def pixel_fuzz_bin(tmp_path_factory):
+    out = str(tmp_path_factory.mktemp("pixfuzz") / "pixel_cone_fuzz")
+    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", out, os.path.join(HERE, "pixel_cone_fuzz.c"), "-lm"],
+                   check=True)
+    return out
+
+
+def test_pixel_margin_matches_kernel():
+    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    assert "const float margin = (M * 0x1.0p-20f) * __builtin_amdgcn_rsqf(dnc);" in src
+    assert "1.0f + 0x1.0p-22f, 0x1.0p-21f + margin));" in src
+    fz = open(os.path.join(HERE, "pixel_cone_fuzz.c")).read()
+    assert "const float margin = (M * 0x1.0p-20f) * rsq(dnc);" in fz
+
+
+@pytest.mark.parametrize("f64", [0, 1], ids=["f32", "f64"])
+def test_pixel_cone_contains_every_ray(pixel_fuzz_bin, f64):
+    """Per-pixel camera cones (pixel_list): every primary ray of the pixel, as computed in T, lies
+    inside the cone (worst case well under a quarter of the pixel margin), and every sphere some ray
+    of the pixel hits (Q1, root2 or scalar test) passes the cone's cull."""
+    r = subprocess.run([pixel_fuzz_bin, "1500000", str(f64), str(0x9E3779B97F4A7C15 + f64)], capture_output=True,
+                       text=True, timeout=300)
+    fields = r.stdout.split()
+    outside = int(fields[fields.index("outside") + 1])
+    misses = int(fields[fields.index("misses") + 1])
+    hits = int(fields[fields.index("hits") + 1])
+    worst = float(fields[-1])
+    assert r.returncode == 0 and outside == 0 and misses == 0, r.stdout
+    assert hits > 1000000, r.stdout
+    assert worst < 0.25, r.stdout
+
+
+@pytest.fixture(scope="module")
 def box_fuzz_bin(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("boxfuzz") / "box_cull_fuzz")
     subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", out, os.path.join(HERE, "box_cull_fuzz.c"), "-lm"],

@@ -616,3 +616,20 @@ def test_cone_cull_dense_tiny_spheres(renderer, flags):
     flat = rt.FlatScene(c, r, rng.integers(0, 3, n).astype(np.uint32), mats)
     lin, st = assert_parity(renderer, flat, cam_for(64, 36), 8, 16, flags)
     assert st.ray_segments > 64 * 36 * 16 * 1.05   # some primary rays really hit the cloud
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_pixel_lists_overflow_and_straddle(renderer, flags):
+    """Per-pixel camera candidate lists (pixel_list): pixels whose cone passes more spheres than a list
+    holds (a file of 12 spheres along the view axis, and pixels crossing it) fall back to the per-batch
+    sweep; the rest use their lists, with spp 100 batches straddling two pixels.  Bit parity."""
+    o = np.array(rt.MAIN_CAMERA["center"])
+    fwd = -o / np.linalg.norm(o)
+    c = [o + fwd * (3.0 + 2.5 * k) for k in range(12)]
+    r = [0.05 + 0.01 * k for k in range(12)]
+    rng = np.random.default_rng(23)
+    for _ in range(60):
+        c.append(rng.uniform(-6, 6, 3) * np.array([1, 0.4, 1])); r.append(rng.uniform(0.2, 0.9))
+    mats = [rt.Lambertian((0.7, 0.6, 0.5)), rt.Metal((0.9, 0.9, 0.9), 0.1), rt.Dielectric(1.5, False)]
+    flat = rt.FlatScene(np.array(c), np.array(r), rng.integers(0, 3, len(r)).astype(np.uint32), mats)
+    assert_parity(renderer, flat, cam_for(31, 17), 50, 100, flags)
