@@ -60,6 +60,8 @@
                             defined(RT_EXP_NO_PARK) || defined(RT_EXP_PARKC_ALL) || defined(RT_EXP_DUP_FINISH) ||    \
                             defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
+                            defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
+                            defined(RT_EXP_DUP_MEGABOX) ||                                                         \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -355,7 +357,7 @@ __device__ __forceinline__ void sphere_loop(cptr<T> f, uint32_t ng, F&& group) {
 // (the one-wait-state packed-FP32 read hazard the compiler pads with s_nop).  14 packed ops, then
 // v_and3 + v_bitop3 on the sign bits.
 __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 K0, f2 K1, f2 K2, f2 K3, uint32_t& s0,
-                                                 uint32_t& s1) {
+                                                 uint32_t& s1, f2* D = nullptr) {
     const f2 cx0 = {cur.v[0], cur.v[1]}, cy0 = {cur.v[2], cur.v[3]}, cz0 = {cur.v[4], cur.v[5]}, rr0 = {cur.v[6], cur.v[7]};
     const f2 cx1 = {cur.v[8], cur.v[9]}, cy1 = {cur.v[10], cur.v[11]}, cz1 = {cur.v[12], cur.v[13]}, rr1 = {cur.v[14], cur.v[15]};
     f2 a0, b0, a1, b1, r0, r1;
@@ -381,6 +383,7 @@ __device__ __forceinline__ uint32_t filter_group(const SphGroup<float>& cur, f2 
     // same per sphere pair, un-negated (sign clear iff a sphere of the pair passes)
     s0 = __float_as_uint(r0.x) & __float_as_uint(r0.y);
     s1 = __float_as_uint(r1.x) & __float_as_uint(r1.y);
+    if (D) { D[0] = r0; D[1] = r1; }   // per sphere (fp64 rays: exact tests per sphere)
     return ~(s0 & s1);
 }
 
@@ -759,8 +762,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             return box_mask(g, B0, C1, C2, C3, C4, btf());
         };
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
-        // the sphere pairs set in `pairs` (bit q: spheres 4g+2q, 4g+2q+1; wave-uniform).
-        auto exact4 = [&](uint32_t g, uint32_t pairs = 3u) {
+        // the sphere pairs set in `pairs` (fp32, bit q: spheres 4g+2q, 4g+2q+1; fp64, bit j: sphere
+        // 4g+j; wave-uniform).
+        auto exact4 = [&](uint32_t g, uint32_t pairs = sizeof(T) == 4 ? 3u : 15u) {
             KSTAT(0);
             if constexpr (sizeof(T) == 4) {
                 // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two
@@ -794,7 +798,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 T hb[4], disc[4];
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j) {
-                    if (!((pairs >> (j >> 1)) & 1u)) continue;
+                    if (!((pairs >> j) & 1u)) continue;
                     const T* v = j < 2 ? &c0.v[4 * j] : &c1.v[4 * (j - 2)];
                     const V3<T> oc = mk(o.x - v[0], o.y - v[1], o.z - v[2]);   // :252
                     if constexpr (SCALAR) {                                    // objects.rs:217-222
@@ -810,7 +814,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 const uint32_t sv[4] = {si.x, si.y, si.z, si.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
-                    if (((pairs >> (j >> 1)) & 1u) && cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
+                    if (((pairs >> j) & 1u) && cand_f(hb[j], disc[j])) hit(hb[j], disc[j], sv[j]);
             }
         };
         // fp32, scene-frame filter groups (not MEGA): the exact test of a taken group takes the centres
@@ -869,8 +873,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // the always-exact groups; fp32 skips a pair of dummies at the end (the ground sphere's group
         // at config C: ground + 3 dummies); in fp64 the variable pair mask costs VGPR spills at W4
         for (uint32_t g = 0; g < nxg; ++g) {
-            const uint32_t pr = sizeof(T) == 4 && 4u * g + 2u >= qa.n_xs ? 1u : 3u;
-            n_exact += pr == 3u ? 4u : 2u;
+            const uint32_t pr = sizeof(T) == 4 ? (4u * g + 2u >= qa.n_xs ? 1u : 3u) : 15u;
+            n_exact += pr == 1u ? 2u : 4u;
             exact4(g, pr);
         }
         // Three levels: super boxes (4 clusters each, 4 per group) per chunk of 32 supers, then the
@@ -885,7 +889,12 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             KSTAT(5);
             ++n_box;
             uint32_t mask;
-            if constexpr (MEGA) mask = lmask(load_lbox((cptr<float>)__builtin_assume_aligned(qa.lclb, 64), sup));
+            if constexpr (MEGA) {
+#ifdef RT_EXP_DUP_CLBOX   // timing experiment: the cluster-box test twice (same result)
+                { uint32_t sup2 = sup; asm volatile("" : "+s"(sup2)); const uint32_t m2 = lmask(load_lbox((cptr<float>)__builtin_assume_aligned(qa.lclb, 64), sup2)); asm volatile("" :: "s"(m2)); }
+#endif
+                mask = lmask(load_lbox((cptr<float>)__builtin_assume_aligned(qa.lclb, 64), sup));
+            }
             else mask = box_mask(load_box(ft, sup), B0, B1, B2, B3, B4, btf());
             while (mask != 0u) {
                 const uint32_t kc = 4u * sup + (uint32_t)__builtin_ctz(mask);   // cluster
@@ -927,12 +936,24 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     uint32_t s0, s1;
                     // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
                     // rejects them as well (the filter passes every sphere the reference can hit).
-                    if (__ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1))) != 0ull) {
+#ifdef RT_EXP_DUP_FILTER   // timing experiment: the filter of each walked group twice (same result)
+                    { f2 M0 = L0; asm volatile("" : "+v"(M0)); uint32_t a0, a1; const uint32_t r2 = filter_group(cur, M0, L1, L2, L3, a0, a1); asm volatile("" :: "v"(r2), "v"(a0), "v"(a1)); }
+#endif
+                    f2 Dv[2];
+                    if (__ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1, sizeof(T) == 8 ? Dv : nullptr))) != 0ull) {
                         // only the sphere pairs some lane passes (one compare each, taken groups
-                        // only; fp64 too since the ray left scratch memory: +1.0 % at C)
-                        const uint32_t pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) |
-                                               (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
-                        n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
+                        // only; fp64 too since the ray left scratch memory: +1.0 % at C).  fp64 rays
+                        // (no packed ops): only the spheres some lane passes.
+                        uint32_t pairs;
+                        if constexpr (sizeof(T) == 4) {
+                            pairs = (__ballot(!is_cand(s0)) != 0ull ? 1u : 0u) | (__ballot(!is_cand(s1)) != 0ull ? 2u : 0u);
+                            n_exact += 2u * (uint32_t)__builtin_popcount(pairs);
+                        } else {
+                            auto ps = [](float D) -> bool { return (int32_t)__float_as_uint(D) >= 0; };   // D >= +0
+                            pairs = (__ballot(ps(Dv[0].x)) != 0ull ? 1u : 0u) | (__ballot(ps(Dv[0].y)) != 0ull ? 2u : 0u) |
+                                    (__ballot(ps(Dv[1].x)) != 0ull ? 4u : 0u) | (__ballot(ps(Dv[1].y)) != 0ull ? 8u : 0u);
+                            n_exact += (uint32_t)__builtin_popcount(pairs);
+                        }
 #ifndef RT_EXP_NO_XREC
                         if constexpr (sizeof(T) == 4 && !MEGA && !CAMT) exact4f(cur, g0 + g, pairs);
                         else
@@ -953,6 +974,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
             // the supers of one passing mega
             auto walk_mega = [&](uint32_t nd) {
                 ++n_box;
+#ifdef RT_EXP_DUP_SUPBOX   // timing experiment: the super-box test twice (same result)
+                { uint32_t nd2 = nd; asm volatile("" : "+s"(nd2)); const uint32_t m2 = lmask(load_lbox(ls, nd2)); asm volatile("" :: "s"(m2)); }
+#endif
                 uint32_t smask = lmask(load_lbox(ls, nd));
                 if (4u * nd + 4u > ntop) smask &= (1u << (ntop - 4u * nd)) - 1u;   // padding supers
                 while (smask != 0u) {
@@ -1006,6 +1030,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
                             lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
                                 KSTAT(5);
+#ifdef RT_EXP_DUP_MEGABOX   // timing experiment: the mega-box tests twice (same result)
+                                { LBoxGroup c2 = cur; asm volatile("" : "+s"(c2.v[0])); const uint32_t m2 = lmask(c2); asm volatile("" :: "s"(m2)); }
+#endif
                                 tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
                             });
                         tm &= valid;
