@@ -61,7 +61,7 @@
                             defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
                             defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
-                            defined(RT_EXP_DUP_MEGABOX) ||                                                         \
+                            defined(RT_EXP_DUP_MEGABOX) || defined(RT_EXP_SMATS) || defined(RT_EXP_EARLYLD) ||     \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -128,6 +128,7 @@ template <typename T> struct KParams {
     uint32_t n_groups;
     const uint32_t* smat;      // [n] material index
     const MatT<T>* mats;
+    const MatT<T>* smats;      // [n] each sphere's material record (mats[smat[i]]: one gather, not two)
     uint32_t n_spheres;
     uint32_t W, H;
     double rW, rH;             // RN(1/W), RN(1/H) for div_dim (0: divide)
@@ -940,7 +941,9 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     { f2 M0 = L0; asm volatile("" : "+v"(M0)); uint32_t a0, a1; const uint32_t r2 = filter_group(cur, M0, L1, L2, L3, a0, a1); asm volatile("" :: "v"(r2), "v"(a0), "v"(a1)); }
 #endif
                     f2 Dv[2];
-                    if (__ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1, sizeof(T) == 8 ? Dv : nullptr))) != 0ull) {
+                    const unsigned long long fpass = __ballot(is_cand(filter_group(cur, L0, L1, L2, L3, s0, s1, sizeof(T) == 8 ? Dv : nullptr)));
+                    KSTAT(7, (uint32_t)__popcll(fpass));   // lanes with a candidate in this group
+                    if (fpass != 0ull) {
                         // only the sphere pairs some lane passes (one compare each, taken groups
                         // only; fp64 too since the ray left scratch memory: +1.0 % at C).  fp64 rays
                         // (no packed ops): only the spheres some lane passes.
@@ -1371,6 +1374,20 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
 template <typename T, bool SCALAR>
 __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy, uint32_t pix, uint32_t sid,
                                          uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
+#ifdef RT_EXP_EARLYLD
+    // the hit sphere's centre and material record, requested before the Philox block (their latency
+    // overlaps it)
+    V3<T> hc = mk(T(0), T(0), T(0));
+    T hr = T(1.0);
+    MatT<T> hm{};
+    if (!cam) {
+        const auto& qe = *cold_args<T>();
+        const T* sg = qe.cen + 4 * hit_i;
+        hc = mk(sg[0], sg[1], sg[2]);
+        if constexpr (SCALAR) hr = sg[3];
+        hm = qe.smats[hit_i];
+    }
+#endif
     const U4 r = [&] {
         const auto& q0 = *cold_args<T>();
         return philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
@@ -1407,11 +1424,16 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         vec = sub(pc, base);
         l2 = len2(vec);                                   // unit(): Vec3::length (geometry.rs:106-112)
     } else {
-        const T* sg = q.cen + 4 * hit_i;
         base = mk(o.x + d.x * hit_t, o.y + d.y * hit_t, o.z + d.z * hit_t);   // at_t
+#ifdef RT_EXP_EARLYLD
+        vec = sub(base, hc);                             // normal = at_t(t) - center (objects.rs:279-280)
+        if constexpr (SCALAR) rad = hr;
+#else
+        const T* sg = q.cen + 4 * hit_i;
         vec = sub(base, mk(sg[0], sg[1], sg[2]));        // normal = at_t(t) - center (objects.rs:279-280)
-        l2 = pk_len2(vec);
         if constexpr (SCALAR) rad = sg[3];
+#endif
+        l2 = pk_len2(vec);
     }
     const T len = (SCALAR && !cam) ? rad : sqrt(l2);
     const V3<T> u = mk(vec.x / len, vec.y / len, vec.z / len);
@@ -1424,7 +1446,13 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
     V3<T> nrm = u;
     const bool front = (SCALAR ? dot(d, nrm) : pk_dot(d, nrm)) < T(0.0);
     if (!front) nrm = neg(nrm);
+#if defined(RT_EXP_EARLYLD)
+    const MatT<T> m = hm;
+#elif defined(RT_EXP_SMATS)
+    const MatT<T> m = q.smats[hit_i];
+#else
     const MatT<T> m = q.mats[q.smat[hit_i]];
+#endif
     V3<T> nd;
     if (m.kind != RT_DIELECTRIC) {
         // One random_unit_vector for both kinds (a wave usually holds both: one evaluation, not two).
@@ -1579,7 +1607,7 @@ enum Mode : int {
 };
 
 // Per-wave scratch of trace_paths (HBM layout): the position map of the pixel being
-// reduced (P entries, u16 -- u32 past 65532 positions: the sample whose value position q holds at the
+// reduced (P entries, u16 -- u32 past 32764 positions: the sample whose value position q holds at the
 // final read, all ones = none), then kSlots record regions indexed by sample: y[P] (T, the primary
 // ray's y), c[P] (3 T, AoS: one dwordx3 store per termination), e[P] (u8 -- u32 when depth > 254: the
 // termination bounce).  In the V1 and scalar modes c holds each sample's final value (colour x sky of
@@ -1589,14 +1617,21 @@ template <typename T> struct PScratch {
     char* base;        // wave-uniform
     uint32_t P, vbytes, sbytes, wide;   // wide: bit 0 = u32 e, bit 1 = u32 map
     static constexpr uint32_t kNone = 0xFFFFFFFFu;
+    // A map entry is a sample index, with kWhite set when that sample hit the sky at bounce 0: its
+    // colour is white, so it wrote no colour record (terminate) and the reduction reads none.  u16
+    // entries keep the flag in bit 15 (P <= 32764, so no flagged index is 0xFFFF).
+    static constexpr uint32_t kWhite = 0x80000000u;
+    __device__ __forceinline__ static uint32_t from16(uint32_t m) {
+        return m == 0xFFFFu ? kNone : (m & 0x7FFFu) | ((m & 0x8000u) << 16);
+    }
+    __device__ __forceinline__ static uint16_t to16(uint32_t v) { return (uint16_t)((v & 0x7FFFu) | ((v >> 16) & 0x8000u)); }
     __device__ __forceinline__ uint32_t map(uint32_t q) const {
         if (wide & 2u) return *(const uint32_t*)(base + 4u * q);
-        const uint32_t m = *(const uint16_t*)(base + 2u * q);
-        return m == 0xFFFFu ? kNone : m;
+        return from16(*(const uint16_t*)(base + 2u * q));
     }
     __device__ __forceinline__ void set_map(uint32_t q, uint32_t smp) const {
         if (wide & 2u) *(uint32_t*)(base + 4u * q) = smp;
-        else *(uint16_t*)(base + 2u * q) = (uint16_t)smp;
+        else *(uint16_t*)(base + 2u * q) = to16(smp);
     }
     __device__ __forceinline__ T& y(uint32_t s, uint32_t i) const {
         return *(T*)(base + vbytes + s * sbytes + i * (uint32_t)sizeof(T));
@@ -1679,8 +1714,8 @@ __device__ __forceinline__ bool guided_block(uint32_t np, uint32_t T, uint32_t G
     return false;
 }
 
-// PScratch sizes: the map (u16, u32 past 65532 positions), the records (e u8, u32 when depth > 254).
-__host__ __device__ inline uint32_t paths_wide(uint32_t P, uint32_t depth) { return (depth > 254u ? 1u : 0u) | (P > 65532u ? 2u : 0u); }
+// PScratch sizes: the map (u16, u32 past 32764 positions), the records (e u8, u32 when depth > 254).
+__host__ __device__ inline uint32_t paths_wide(uint32_t P, uint32_t depth) { return (depth > 254u ? 1u : 0u) | (P > 32764u ? 2u : 0u); }
 __host__ __device__ inline uint32_t paths_vbytes(uint32_t P, uint32_t wide, bool v3) {
     return v3 ? (8u * P + 255u) & ~255u   // vectorized3: slot -> sample map + the swap tables (finish_pixel)
               : (P * ((wide & 2u) ? 4u : 2u) + 255u) & ~255u;
@@ -1714,7 +1749,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     constexpr uint32_t kNone = PScratch<T>::kNone;
     const bool lm = kLMapCap > 0u && lmap != nullptr && P <= kLMapCap;   // wave-uniform
     auto set_map = [&](uint32_t qq, uint32_t smp) {
-        if (lm) lmap[qq] = (uint16_t)smp;
+        if (lm) lmap[qq] = PScratch<T>::to16(smp);
         else sc.set_map(qq, smp);
     };
     // Map init: no position holds a terminated sample's value yet (survivors and never-written
@@ -1775,7 +1810,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             const uint32_t y = (uint32_t)__shfl_up((int)pre, o);
             if (lane >= o) pre += y;
         }
-        const uint32_t n_l = spp - (pre - H), nn_l = spp - pre;   // n_k, n_{k+1} for k = lane
+        const uint32_t nn_l = spp - pre;   // n_{k+1} for k = lane
         uint32_t cge = 0, ceq = 0;   // lane k: samples of the earlier chunks with e >= k, e == k
         for (uint32_t b = 0; b < spp; b += 512u) {   // the samples in order, 64 at a time
             uint32_t ev[8];
@@ -1790,17 +1825,16 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const uint32_t i = b + 64u * u + lane, e = ev[u];
                 const bool in = i < spp, ret = e < K;
                 unsigned long long rem = __ballot(ret);
-                uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nk = 0, nn = 0;
+                uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nn = 0;
                 while (rem != 0ull) {   // one pass per distinct bounce k among the chunk's retiring lanes
                     const uint32_t k = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(rem));
                     const unsigned long long bge = __ballot(in && e >= k), beq = __ballot(e == k);
                     const uint32_t cnt = (uint32_t)__popcll(beq);
                     const uint32_t cg = __builtin_amdgcn_readlane(cge, (int)k), cq = __builtin_amdgcn_readlane(ceq, (int)k);
-                    const uint32_t n0 = __builtin_amdgcn_readlane(n_l, (int)k), n1 = __builtin_amdgcn_readlane(nn_l, (int)k);
+                    const uint32_t n1 = __builtin_amdgcn_readlane(nn_l, (int)k);
                     if (e == k) {
                         pold = cg + (uint32_t)__popcll(bge & lt_mask);
                         pnew = n1 + cq + (uint32_t)__popcll(beq & lt_mask);
-                        nk = n0;
                         nn = n1;
                     }
                     if (lane <= k) gadd += cnt;   // lane j: this chunk's #{e >= j}
@@ -1811,13 +1845,17 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 ceq += hc;
                 const uint32_t ek = ret ? e : 0u;
                 if (ret) {
-                    const uint32_t Lk = (nk + 3u) / 4u, Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
-                    const uint32_t lo = 4u * Lnext, hi = 4u * Lk;   // positions retiring at bounce e
+                    const uint32_t Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
+                    // positions [lo, 4 ceil(n_k / 4)) retire at bounce e; pold and pnew are below n_k <= 4 Lk (pold
+                    // counts the earlier samples with e >= k, pnew = n_{k+1} + the earlier ones with
+                    // e == k), so only lo bounds them
+                    const uint32_t lo = 4u * Lnext;
                     const bool U = q.s_sel == (ek & 1u);
-                    const bool w_old = U && pold >= lo && pold < hi;
-                    const bool w_new = !U || pnew < lo || pnew >= hi;
-                    if (w_old || w_new) set_map(w_old ? pold : pnew, i);
-                    if (w_old && w_new) set_map(pnew, i);
+                    const bool w_old = U && pold >= lo;
+                    const bool w_new = !U || pnew < lo;
+                    const uint32_t iw = ek == 0u ? (i | PScratch<T>::kWhite) : i;
+                    if (w_old || w_new) set_map(w_old ? pold : pnew, iw);
+                    if (w_old && w_new) set_map(pnew, iw);
                 }
             }
         }
@@ -1886,7 +1924,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             wave_mem_sync();
         }
     }
-    uint32_t n = spp, Lcur = C, kb = 0xFFFFFFFFu;
+    uint32_t n = spp, kb = 0xFFFFFFFFu;
     for (uint32_t k = 0; k < (MODE == kModeV2 && !replayed ? K : 0u); ++k) {
         if (kb == 0xFFFFFFFFu || k - kb >= 64u) {   // histogram of e over [k, k+64)
             kb = k;
@@ -1903,7 +1941,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         const uint32_t n_next = n - m;
         const uint32_t Lnext = (k + 1 == depth) ? 0u : (n_next + 3u) / 4u;
         if (m > 0) {
-            const uint32_t lo = 4u * Lnext, hi = 4u * Lcur;   // positions retiring at bounce k
+            const uint32_t lo = 4u * Lnext;   // positions [lo, 4 ceil(n_k / 4)) retire at bounce k
             const bool U = q.s_sel == (k & 1u);                 // final read = this bounce's unsorted buffer
             uint32_t cge = 0, ceq = 0;
             for (uint32_t b = 0; b < spp && ceq < m; b += 64u) {
@@ -1914,18 +1952,18 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 if (eq) {
                     const uint32_t pold = cge + (uint32_t)__popcll(bge & lt_mask);
                     const uint32_t pnew = n_next + ceq + (uint32_t)__popcll(beq & lt_mask);
-                    const bool w_old = U && pold >= lo && pold < hi;
-                    const bool w_new = !U || pnew < lo || pnew >= hi;
+                    const bool w_old = U && pold >= lo;   // pold, pnew < n_k <= hi (as above)
+                    const bool w_new = !U || pnew < lo;
                     // At most one position except when the old one retires now and the new one later.
-                    if (w_old || w_new) set_map(w_old ? pold : pnew, i);
-                    if (w_old && w_new) set_map(pnew, i);
+                    const uint32_t iw = k == 0u ? (i | PScratch<T>::kWhite) : i;
+                    if (w_old || w_new) set_map(w_old ? pold : pnew, iw);
+                    if (w_old && w_new) set_map(pnew, iw);
                 }
                 cge += (uint32_t)__popcll(bge);
                 ceq += (uint32_t)__popcll(beq);
             }
         }
         n = n_next;
-        Lcur = Lnext;
     }
     wave_mem_sync();
     // Final reduction in the reference's order: per lane l, chunks j = 0..C-1 from +0.0
@@ -1985,16 +2023,15 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                     }
                 } else if constexpr (MODE == kModeV2) {
                     uint32_t m;
-                    if (lm) {
-                        m = lmap[qq];
-                        if (m == 0xFFFFu) m = kNone;
-                    } else {
-                        m = sc.map(qq);
-                    }
+                    if (lm) m = PScratch<T>::from16(lmap[qq]);
+                    else m = sc.map(qq);
                     if (m != kNone) {
-                        const C3<T> cm = sc.c(s, m);
+                        // a bounce-0 sky hit (kWhite) wrote no record: white x sky.  Branch-free (the
+                        // record slot is read anyway and replaced by white: a branch cost 0.8 % at C)
+                        const bool wh = (m & PScratch<T>::kWhite) != 0u;
+                        const C3<T> cm = sc.c(s, m & ~PScratch<T>::kWhite);
                         const V3<T> sk = sky(sc.y(s, qq));
-                        vr = cm.x * sk.x; vg = cm.y * sk.y; vb = cm.z * sk.z;
+                        vr = (wh ? T(1.0) : cm.x) * sk.x; vg = (wh ? T(1.0) : cm.y) * sk.y; vb = (wh ? T(1.0) : cm.z) * sk.z;
                     }
                 } else {
                     const C3<T> cm = sc.c(s, qq);
@@ -2219,8 +2256,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             sc.set_e(t_slot, t_sid, e);
             if (MODE == kModeV2) {
                 // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
-                // the copies into them raised the register peak (spills in the sphere sweeps)
-                if (skyhit) sc.store_c(t_slot, t_sid, tc.x, tc.y, tc.z);
+                // the copies into them raised the register peak (spills in the sphere sweeps).  A sky
+                // hit at bounce 0 is white: no record (its map entry carries kWhite, finish_pixel)
+                if (skyhit && e != 0u) sc.store_c(t_slot, t_sid, tc.x, tc.y, tc.z);
             } else {   // own value: colour x sky of the escaping ray's direction (:365-370 / :283-292), or black
                 V3<T> v = mk(T(0.0), T(0.0), T(0.0));
                 if (skyhit) { const V3<T> sk = sky(td.y); v = mk(tc.x * sk.x, tc.y * sk.y, tc.z * sk.z); }
@@ -2513,6 +2551,7 @@ struct rt_context {
     uint32_t n_top = 0, n_xg = 0, n_xs = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
     void* mat64 = nullptr; void* mat32 = nullptr;
+    void* smat64 = nullptr; void* smat32 = nullptr;   // per-sphere material records
     uint32_t* smat = nullptr;
     uint32_t n_spheres = 0, n_materials = 0;
     unsigned long long* segs = nullptr;
@@ -2620,6 +2659,8 @@ static void free_scene(rt_context* c) {
     c->ridx = nullptr;
     c->n_top = c->n_xg = c->n_xs = 0;
     (void)hipFree(c->smat);
+    (void)hipFree(c->smat64); (void)hipFree(c->smat32);
+    c->smat64 = c->smat32 = nullptr;
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
     c->smat = nullptr;
     c->n_spheres = c->n_materials = 0;
@@ -3325,6 +3366,14 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
     if ((rc = up(&c->mat32, m32.data(), m32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
     if ((rc = up((void**)&c->smat, sm.data(), sm.size() * sizeof(uint32_t))) != RT_OK) return rc;
+    {
+        std::vector<MatT<double>> s64(sm.size());
+        std::vector<MatT<float>> s32(sm.size());
+        for (size_t i = 0; i < sm.size(); ++i)
+            if (sm[i] < m64.size()) { s64[i] = m64[sm[i]]; s32[i] = m32[sm[i]]; }
+        if ((rc = up(&c->smat64, s64.data(), s64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
+        if ((rc = up(&c->smat32, s32.data(), s32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
+    }
     c->n_spheres = s->n_spheres;
     c->n_materials = s->n_materials;
     return RT_OK;
@@ -3434,6 +3483,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     }
     p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
     p.smat = c->smat;
+    p.smats = (const MatT<T>*)(f64 ? c->smat64 : c->smat32);
     p.n_spheres = c->n_spheres;
     p.W = cam->image_width; p.H = cam->image_height;
     p.rW = p.W < (1u << 20) ? 1.0 / (double)p.W : 0.0;   // div_dim
@@ -3592,10 +3642,10 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
         for (int j = 0; j < 8; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
     if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
         fprintf(stderr, "rt_kstats: general taken_groups %llu sweeps %llu clusters %llu top_groups %llu  camera "
-                "candidates %llu sweeps %llu  finish_pixel %llu\n",
+                "candidates %llu sweeps %llu  finish_pixel %llu  filter_lanes_passing %llu\n",
                 (unsigned long long)kst[0], (unsigned long long)kst[1], (unsigned long long)kst[4],
                 (unsigned long long)kst[5], (unsigned long long)kst[2], (unsigned long long)kst[3],
-                (unsigned long long)kst[6]);
+                (unsigned long long)kst[6], (unsigned long long)kst[7]);
     for (int i = 0; i < kSegShards; ++i) {
         total += segs[(size_t)i * kSegStride];
         slots += segs[(size_t)i * kSegStride + 1];

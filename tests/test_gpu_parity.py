@@ -99,9 +99,12 @@ def test_fp64_2048(renderer, scene_100):
 
 
 def test_wide_records(renderer, scene_100):
-    """The scratch formats' wide variants (PScratch): more than 65532 positions per pixel take a u32
-    position map, depth > 254 takes u32 termination bounces."""
+    """The scratch formats' wide variants (PScratch): more than 32764 positions per pixel take a u32
+    position map (u16 entries keep the bounce-0 "white" flag in bit 15), depth > 254 takes u32
+    termination bounces.  Both sides of the map's boundary, in both precisions."""
     assert_parity(renderer, scene_100, cam_for(2, 1), 50, 70001, abi.RT_FLAG_F32)   # P = 70004 > 65532
+    assert_parity(renderer, scene_100, cam_for(2, 1), 50, 32761, abi.RT_FLAG_F32)   # P = 32764: u16
+    assert_parity(renderer, scene_100, cam_for(2, 1), 50, 32765, 0)                 # P = 32768: u32
     assert_parity(renderer, scene_100, cam_for(16, 9), 300, 16, 0)                 # depth 300 > 254
 
 
