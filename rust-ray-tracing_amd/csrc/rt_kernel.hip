@@ -61,7 +61,7 @@
                             defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
                             defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
-                            defined(RT_EXP_DUP_MEGABOX) || defined(RT_EXP_SMATS) || defined(RT_EXP_EARLYLD) ||     \
+                            defined(RT_EXP_DUP_MEGABOX) || \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -126,9 +126,7 @@ template <typename T> struct KParams {
     const T* sph;              // grouped sphere records (layout above); r^2 = r.powi(2) in T (objects.rs:256)
     const T* cen;              // [n][4] = cx, cy, cz, r^2 (AoS, finalize gather)
     uint32_t n_groups;
-    const uint32_t* smat;      // [n] material index
-    const MatT<T>* mats;
-    const MatT<T>* smats;      // [n] each sphere's material record (mats[smat[i]]: one gather, not two)
+    const MatT<T>* mats;       // [n] each sphere's material record, materials[material[i]] (one gather)
     uint32_t n_spheres;
     uint32_t W, H;
     double rW, rH;             // RN(1/W), RN(1/H) for div_dim (0: divide)
@@ -1374,20 +1372,6 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
 template <typename T, bool SCALAR>
 __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy, uint32_t pix, uint32_t sid,
                                          uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
-#ifdef RT_EXP_EARLYLD
-    // the hit sphere's centre and material record, requested before the Philox block (their latency
-    // overlaps it)
-    V3<T> hc = mk(T(0), T(0), T(0));
-    T hr = T(1.0);
-    MatT<T> hm{};
-    if (!cam) {
-        const auto& qe = *cold_args<T>();
-        const T* sg = qe.cen + 4 * hit_i;
-        hc = mk(sg[0], sg[1], sg[2]);
-        if constexpr (SCALAR) hr = sg[3];
-        hm = qe.smats[hit_i];
-    }
-#endif
     const U4 r = [&] {
         const auto& q0 = *cold_args<T>();
         return philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
@@ -1425,14 +1409,9 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         l2 = len2(vec);                                   // unit(): Vec3::length (geometry.rs:106-112)
     } else {
         base = mk(o.x + d.x * hit_t, o.y + d.y * hit_t, o.z + d.z * hit_t);   // at_t
-#ifdef RT_EXP_EARLYLD
-        vec = sub(base, hc);                             // normal = at_t(t) - center (objects.rs:279-280)
-        if constexpr (SCALAR) rad = hr;
-#else
         const T* sg = q.cen + 4 * hit_i;
         vec = sub(base, mk(sg[0], sg[1], sg[2]));        // normal = at_t(t) - center (objects.rs:279-280)
         if constexpr (SCALAR) rad = sg[3];
-#endif
         l2 = pk_len2(vec);
     }
     const T len = (SCALAR && !cam) ? rad : sqrt(l2);
@@ -1446,13 +1425,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
     V3<T> nrm = u;
     const bool front = (SCALAR ? dot(d, nrm) : pk_dot(d, nrm)) < T(0.0);
     if (!front) nrm = neg(nrm);
-#if defined(RT_EXP_EARLYLD)
-    const MatT<T> m = hm;
-#elif defined(RT_EXP_SMATS)
-    const MatT<T> m = q.smats[hit_i];
-#else
-    const MatT<T> m = q.mats[q.smat[hit_i]];
-#endif
+    const MatT<T> m = q.mats[hit_i];                     // = materials[material[hit_i]] (objects.rs:296)
     V3<T> nd;
     if (m.kind != RT_DIELECTRIC) {
         // One random_unit_vector for both kinds (a wave usually holds both: one evaluation, not two).
@@ -2550,9 +2523,7 @@ struct rt_context {
     uint32_t n_supc = 0;                              // super records after them (x64; 0: none)
     uint32_t n_top = 0, n_xg = 0, n_xs = 0;
     uint32_t n_groups64 = 0, n_groups32 = 0;
-    void* mat64 = nullptr; void* mat32 = nullptr;
-    void* smat64 = nullptr; void* smat32 = nullptr;   // per-sphere material records
-    uint32_t* smat = nullptr;
+    void* mat64 = nullptr; void* mat32 = nullptr;     // per-sphere material records
     uint32_t n_spheres = 0, n_materials = 0;
     unsigned long long* segs = nullptr;
     uint32_t* err = nullptr;
@@ -2658,11 +2629,7 @@ static void free_scene(rt_context* c) {
     c->rsph64 = c->rsph32 = c->rfsph64 = c->rfsph32 = c->top64 = c->top32 = nullptr;
     c->ridx = nullptr;
     c->n_top = c->n_xg = c->n_xs = 0;
-    (void)hipFree(c->smat);
-    (void)hipFree(c->smat64); (void)hipFree(c->smat32);
-    c->smat64 = c->smat32 = nullptr;
     c->sph64 = c->sph32 = c->mat64 = c->mat32 = c->cen64 = c->cen32 = nullptr;
-    c->smat = nullptr;
     c->n_spheres = c->n_materials = 0;
 }
 
@@ -3363,16 +3330,14 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     HIPCHK(hipMalloc(&c->cull32, (size_t)4 * c->n_cslots * sizeof(float)));
     if ((rc = up(&c->cen64, c64.data(), c64.size() * sizeof(double))) != RT_OK) return rc;
     if ((rc = up(&c->cen32, c32.data(), c32.size() * sizeof(float))) != RT_OK) return rc;
-    if ((rc = up(&c->mat64, m64.data(), m64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
-    if ((rc = up(&c->mat32, m32.data(), m32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
-    if ((rc = up((void**)&c->smat, sm.data(), sm.size() * sizeof(uint32_t))) != RT_OK) return rc;
     {
+        // per-sphere records: next_ray gathers a hit sphere's material in one dependent load
         std::vector<MatT<double>> s64(sm.size());
         std::vector<MatT<float>> s32(sm.size());
         for (size_t i = 0; i < sm.size(); ++i)
             if (sm[i] < m64.size()) { s64[i] = m64[sm[i]]; s32[i] = m32[sm[i]]; }
-        if ((rc = up(&c->smat64, s64.data(), s64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
-        if ((rc = up(&c->smat32, s32.data(), s32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
+        if ((rc = up(&c->mat64, s64.data(), s64.size() * sizeof(MatT<double>))) != RT_OK) return rc;
+        if ((rc = up(&c->mat32, s32.data(), s32.size() * sizeof(MatT<float>))) != RT_OK) return rc;
     }
     c->n_spheres = s->n_spheres;
     c->n_materials = s->n_materials;
@@ -3482,8 +3447,6 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         if (filter_off) p.f_cmax = std::numeric_limits<float>::infinity();
     }
     p.mats = (const MatT<T>*)(f64 ? c->mat64 : c->mat32);
-    p.smat = c->smat;
-    p.smats = (const MatT<T>*)(f64 ? c->smat64 : c->smat32);
     p.n_spheres = c->n_spheres;
     p.W = cam->image_width; p.H = cam->image_height;
     p.rW = p.W < (1u << 20) ? 1.0 / (double)p.W : 0.0;   // div_dim
