@@ -25,6 +25,9 @@ roofline: the trace kernel is bound by VALU issue (no MFMA; HBM 
 --gpus N > 1 without a launcher (no RANK in the environment): bench.py starts N ranks itself, as a
   child `python -m torch.distributed.run --nproc-per-node N bench.py ...` (never exec), and exits with
   its return code; a rank whose initialised world size is not --gpus exits non-zero.
+--schedule dynamic: instead of one static row shard per rank, the ranks pull chunks (rows j, j+M, ...)
+  from a counter in the process group's store, the reference's shared tile channel; every rank writes
+  its chunks into a zeroed full frame and one RCCL reduce (sum) assembles the image on rank 0.
 cpu_baseline: the CPU restatement (oracle/, f64, 4-lane packets like PackedRays<4>), built
   -march=native on this host, on every core this process may use (affinity, capped by the cgroup's
   CPU quota), over a bounded strided pixel sample of the same workload.
@@ -58,6 +61,10 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc.json"))
     ap.add_argument("--max-spheres", type=int, default=0, help="experiment: truncate the scene (not a bench line)")
+    ap.add_argument("--schedule", default="static", choices=["static", "dynamic"],
+                    help="static: rank r renders rows r, r+N, ... (one launch); dynamic: ranks pull row-interleaved "
+                         "chunks from a shared queue (the reference's tile channel, renderer.rs:248-296)")
+    ap.add_argument("--chunks", type=int, default=0, help="dynamic schedule: chunks per frame (0 = 4 x ranks)")
     ap.add_argument("--probe-dist", action="store_true",
                     help="launcher rehearsal: set up the ranks and the process group, print the world, no GPU work")
     return ap.parse_args()
@@ -246,8 +253,65 @@ def main():
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
     red_dev = "cuda" if backend == "nccl" else "cpu"
+    dynamic = args.schedule == "dynamic"
+    n_chunks = args.chunks or 4 * world
+    if dynamic:
+        store = parallel.default_store() if dist_on else None
+        frame = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
+        cbufs = [torch.zeros((parallel.rows_max(H, n_chunks), W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    sched = {"steps": 0, "chunks": 0, "pixels": 0}   # dynamic: this leg's claims on this rank
+
+    def step_dynamic(flags, ev=None):
+        """One frame under the dynamic schedule: claim a chunk, launch it, keep at most two chunks queued
+        on the GPU (the host claims the next one only once the one before the last has finished), write
+        each into the zeroed frame, then one reduce (sum: every pixel is nonzero on one rank at most)."""
+        key = f"rt-bench/{sched['steps']}"
+        sched["steps"] += 1
+        q = parallel.TileQueue(store, key, n_chunks) if store is not None else None
+        frame.zero_()
+        if ev:
+            ev[0].record(stream)
+        pend, k = [], 0
+        while True:
+            if q is not None:
+                j = q.claim()
+            else:   # one process: it takes every chunk in order
+                j = k if k < n_chunks else None
+            if j is None:
+                break
+            tr = parallel.chunk_range(W, H, n_chunks, j)
+            buf = cbufs[k % 2]
+            abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tr),
+                                               ctypes.c_void_p(buf.data_ptr()), None, sptr))
+            parallel.place_chunk(frame, buf, H, n_chunks, j)
+            done = torch.cuda.Event()
+            done.record(stream)
+            pend.append(done)
+            if len(pend) >= 2:
+                pend.pop(0).synchronize()
+            sched["chunks"] += 1
+            sched["pixels"] += tr.row_count * W
+            k += 1
+        if ev:
+            ev[1].record(stream)
+        if world > 1:
+            if backend == "nccl":
+                dist.reduce(frame, dst=0, op=dist.ReduceOp.SUM)
+            else:
+                host = frame.cpu()
+                dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+                if rank == 0:
+                    frame.copy_(host)
+        if ev:
+            ev[2].record(stream)
+        if rank == 0:
+            image.copy_(frame)
+        if ev:
+            ev[3].record(stream)
 
     def step(flags, ev=None):
+        if dynamic:
+            return step_dynamic(flags, ev)
         if ev:
             ev[0].record(stream)
         abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tile),
@@ -283,6 +347,7 @@ def main():
         torch.cuda.synchronize()
         abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(abi.RtStats())), allow=(abi.RT_ERR_RANGE,))
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+        sched["chunks"] = sched["pixels"] = 0
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -296,8 +361,9 @@ def main():
         st = abi.RtStats()
         rc = abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(st)), allow=(abi.RT_ERR_RANGE,))
         phase = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / args.steps for i in range(3)]   # ms per step
-        px_s = tile.row_count * W / (phase[0] / 1e3) if phase[0] > 0 else 0.0   # this shard's px/s (renderer.rs:339)
-        mine = [elapsed, phase[0], phase[1], phase[2], float(st.ray_segments), px_s]
+        pix = sched["pixels"] / args.steps if dynamic else tile.row_count * W   # pixels this rank renders per step
+        px_s = pix / (phase[0] / 1e3) if phase[0] > 0 else 0.0   # this rank's px/s (renderer.rs:339)
+        mine = [elapsed, phase[0], phase[1], phase[2], float(st.ray_segments), px_s, pix, sched["chunks"] / args.steps]
         if world > 1:
             t = torch.tensor(mine, dtype=torch.float64, device=red_dev)
             allr = [torch.empty_like(t) for _ in range(world)]
@@ -332,7 +398,7 @@ def main():
                 "brute_force_equiv": {"flop_per_launch": bf, "tflops": bf / launch_s / 1e12,
                                       "x_fp32_peak": bf / launch_s / 1e12 / PEAK_TF["f32"]},
             },
-            "ray_segments_per_sample": st.ray_segments / (tile.row_count * W * spp * args.steps),
+            "ray_segments_per_sample": st.ray_segments / max(1.0, per_rank[rank][6] * spp * args.steps),
             "lane_utilisation": st.ray_segments / max(1, st.lane_slots),
             "bounces_per_pixel": st.bounce_iters / max(1, st.pixels),
             "range_error": rc == abi.RT_ERR_RANGE,
@@ -356,7 +422,7 @@ def main():
             pass
         rl = head["roofline"]
         rl.update(pmc_fields(pmc, vinfo["src_hash"], os.path.relpath(args.pmc, REPO)))
-        rl["algorithmic_bytes"] = tile.row_count * W * 3 + flat.n_spheres * 20   # RGB8 out + the scene (SoA)
+        rl["algorithmic_bytes"] = int(head["per_rank"][rank][6]) * 3 + flat.n_spheres * 20   # RGB8 out + the scene (SoA)
         rl["traffic_over_algorithmic"] = (rl["traffic"] / rl["algorithmic_bytes"]) if rl["traffic"] else None
         line = {
             "metric": "Msamples/s (pixels×spp/s), 1920×1080·512spp·500 spheres; 1/2/4/8 GPU",
@@ -375,9 +441,13 @@ def main():
                 "workload": f"{args.config}: {W}x{H}, {n_sph} spheres (RTIOW-style, seed 0x5EED0001), "
                             f"{spp} spp, {depth} bounces, camera of src/main.rs:51-58",
                 "width": W, "height": H, "spheres": n_sph, "spp": spp, "max_bounces": depth,
-                "parallelism": f"row-interleaved image shards x{world}"
-                               + ((" + RCCL gather" if backend == "nccl" else f" + {backend} gather (rehearsal)")
-                                  if world > 1 else ""),
+                "parallelism": (f"dynamic queue of {n_chunks} row-interleaved chunks over {world} rank(s)"
+                                + ((" + RCCL reduce" if backend == "nccl" else f" + {backend} reduce (rehearsal)")
+                                   if world > 1 else "")) if dynamic else
+                               (f"row-interleaved image shards x{world}"
+                                + ((" + RCCL gather" if backend == "nccl" else f" + {backend} gather (rehearsal)")
+                                   if world > 1 else "")),
+                "schedule": args.schedule,
             },
             "roofline": rl,
             "launch_ms": round(head["launch_ms"], 3),
@@ -399,7 +469,8 @@ def main():
             "imbalance": round(max(rms) / (sum(rms) / len(rms)), 4) if sum(rms) > 0 else None,   # max / mean render
             "rccl_version": (".".join(map(str, torch.cuda.nccl.version())) if dist_on and backend == "nccl" else None),
             "per_rank": [{"rank": r, "wall_s": round(p[0], 4), "render_ms": round(p[1], 3), "gather_ms": round(p[2], 3),
-                          "assemble_ms": round(p[3], 3), "ray_segments": int(p[4]), "px_per_s": round(p[5], 1)}
+                          "assemble_ms": round(p[3], 3), "ray_segments": int(p[4]), "px_per_s": round(p[5], 1),
+                          "pixels": int(p[6]), "chunks": p[7] if dynamic else None}
                          for r, p in enumerate(head["per_rank"])],
         }
         line["build"] = {"library": vinfo["version"], "source_hash": src_hash,

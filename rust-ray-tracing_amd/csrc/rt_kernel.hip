@@ -1662,6 +1662,11 @@ struct IssueState { uint32_t busy, cur, cur_next, cur_pix, cur_row, cur_col, dra
 //     config C: waves on a CU then walk different clusters, and the sphere data thrash the scalar cache.
 constexpr uint32_t kMaxBlock = 16;
 constexpr uint32_t kBlockShare = 24;
+// The counter serves ~90 M claims/s, and the chip runs ~3e10 samples/s: a launch claims at most one
+// block per kClaimSpp samples (G >= kClaimSpp / spp), so claims stay under ~half the counter's rate
+// at any spp.  Without it the share bound took small launches to single pixels: a quarter of config B
+// (128 spp) then made 230 k claims, 2.5 ms of atomics for 1 ms of work (tools/multirank_check.sh).
+constexpr uint32_t kClaimSpp = 640;
 #ifndef RT_EXP_BLOCK_SAMPLES
 #define RT_EXP_BLOCK_SAMPLES 8192
 #endif
@@ -2017,17 +2022,20 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             __builtin_amdgcn_wave_barrier();
             if (lane < 12u) {
-                const uint32_t nu = min(16u, (P - qb) / 4u);
+                const uint32_t nu = min(16u, (P - qb) / 4u);   // wave-uniform; 16 except a short last batch
                 const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
                 T a = accl[lane];
+                if (nu == 16u) {   // a whole batch: plain adds (the guarded form costs a compare and a select each)
 #pragma unroll
-                for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
-                    T v[4];
+                    for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
+                        T v[4];
 #pragma unroll
-                    for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
+                        for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
 #pragma unroll
-                    for (uint32_t u = 0; u < 4u; ++u)
-                        if (u0 + u < nu) a = a + v[u];
+                        for (uint32_t u = 0; u < 4u; ++u) a = a + v[u];
+                    }
+                } else {
+                    for (uint32_t u = 0; u < nu; ++u) a = a + sv[u];
                 }
                 accl[lane] = a;
             }
@@ -3513,10 +3521,12 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
     const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
     if (nblocks > need) nblocks = need;
-    {   // G: the largest power of two <= min(kMaxBlock, kBlockSamples / spp, pixels per wave / kBlockShare)
+    {   // G: the largest power of two <= min(kMaxBlock, kBlockSamples / spp, pixels per wave / kBlockShare),
+        // raised to kClaimSpp / spp (claim rate, below) where the share bound would go under it
         const uint64_t per_wave = (uint64_t)p.n_items / (4u * nblocks);
-        const uint64_t g = std::max<uint64_t>(1u, std::min<uint64_t>({(uint64_t)kMaxBlock, kBlockSamples / spp,
-                                                                      per_wave / kBlockShare}));
+        const uint64_t g = std::max<uint64_t>({1u, std::min<uint64_t>({(uint64_t)kMaxBlock, kBlockSamples / spp,
+                                                                       per_wave / kBlockShare}),
+                                               std::min<uint64_t>((uint64_t)kMaxBlock, (kClaimSpp + spp - 1) / spp)});
         uint32_t G = 1;
         while (2u * G <= g) G *= 2u;
         p.blk_g = G;

@@ -75,3 +75,68 @@ def test_partition_covers_every_row_once():
             rows = sorted(r for k in range(world) for r in parallel.shard_rows(h, world, k))
             assert rows == list(range(h))
             assert max(len(parallel.shard_rows(h, world, k)) for k in range(world)) == parallel.rows_max(h, world)
+
+
+def _dyn_worker(rank, world, port, out_path, n_chunks):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "rust-ray-tracing_amd"))
+    sys.path.insert(0, here)
+    import rt_mi355x as rt
+    from rt_mi355x import parallel
+    from oracle_bind import oracle_render
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
+    q = parallel.TileQueue(parallel.default_store(), "test-tiles/0", n_chunks)
+    frame = np.zeros((H, W, 3), np.float64)
+    segs_total = 0
+    while (j := q.claim()) is not None:
+        tr = parallel.chunk_range(W, H, n_chunks, j)
+        rows = list(parallel.chunk_rows(H, n_chunks, j))
+        assert tr.row_begin == j and tr.row_step == n_chunks and tr.row_count == len(rows)
+        pixels = np.array([r * W + c for r in rows for c in range(W)], np.uint32)
+        _, lin, segs, _ = oracle_render(flat, cam, DEPTH, SPP, SEED, pixels=pixels, threads=1)
+        parallel.place_chunk(frame, lin.reshape(len(rows), W, 3), H, n_chunks, j)
+        segs_total += segs
+    t = torch.from_numpy(frame)
+    dist.reduce(t, dst=0, op=dist.ReduceOp.SUM)   # each pixel is nonzero on one rank at most: x + 0 == x
+    claimed = torch.zeros(n_chunks, dtype=torch.int64)
+    for j in q.claimed:
+        claimed[j] += 1
+    dist.all_reduce(claimed)
+    seg_t = torch.tensor([segs_total], dtype=torch.int64)
+    dist.all_reduce(seg_t)
+    if rank == 0:
+        np.savez(out_path, img=t.numpy(), segs=int(seg_t.item()), claimed=claimed.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_chunks", [(2, 5), (3, 12)])
+def test_dynamic_chunk_queue_bit_identical(tmp_path, world, n_chunks):
+    """bench.py --schedule dynamic's partition: ranks pull row-interleaved chunks from the process
+    group's store (the reference's shared tile channel, renderer.rs:248-296); every chunk is claimed
+    exactly once and the reduced frame equals the single-process render bit for bit."""
+    out = str(tmp_path / "img.npz")
+    mp.spawn(_dyn_worker, args=(world, _free_port(), out, n_chunks), nprocs=world, join=True)
+    import rt_mi355x as rt
+    from oracle_bind import oracle_render
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
+    _, full, segs, _ = oracle_render(flat, cam, DEPTH, SPP, SEED)
+    got = np.load(out)
+    np.testing.assert_array_equal(got["claimed"], np.ones(n_chunks, np.int64))
+    np.testing.assert_array_equal(got["img"], full.reshape(H, W, 3))
+    assert int(got["segs"]) == segs
+
+
+def test_chunks_cover_every_row_once():
+    from rt_mi355x import parallel
+    for h in (1, 7, 1080, 2160):
+        for m in (1, 2, 5, 32):
+            rows = sorted(r for j in range(m) for r in parallel.chunk_rows(h, m, j))
+            assert rows == list(range(h))
+            assert all(parallel.chunk_range(17, h, m, j).row_count == len(parallel.chunk_rows(h, m, j)) for j in range(m))
