@@ -61,7 +61,8 @@
                             defined(RT_EXP_DUP_CAMRAY) || defined(RT_EXP_NO_CAMCULL) || defined(RT_EXP_DUP_CAM) ||   \
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
                             defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
-                            defined(RT_EXP_DUP_MEGABOX) || \
+                            defined(RT_EXP_DUP_MEGABOX) || defined(RT_EXP_DUP_PLIST) || defined(RT_EXP_DUP_REPLAY) || \
+                            defined(RT_EXP_DUP_REDUCE) || \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -1107,6 +1108,18 @@ __device__ __forceinline__ uint32_t wave_max_dpp(uint32_t v) {
     return __builtin_amdgcn_readlane(v, 63);
 }
 
+// Wave-wide inclusive prefix sum of a uint32 through DPP (Hillis-Steele within each row of 16 with
+// zero fill, then row_bcast:15 / row_bcast:31 carry the row totals upwards).
+__device__ __forceinline__ uint32_t wave_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);   // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);   // row_bcast:31
+    return v;
+}
+
 // The cone cull over the sweep layout (whole wave, wave-uniform control flow): calls pass(sl) for every
 // sphere slot whose cone-cull record {w = c - O, rp} the cone with axis a, sin S and cos Cc does not
 // cull (all: every record passes).  Returns the wave-level cone tests run.  xw0, kw0: the first
@@ -1781,15 +1794,20 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
 #if !defined(RT_EXP_OLD_REPLAY)
     if (MODE == kModeV2 && K > 0u && K <= 64u) {
         replayed = true;
-        const uint32_t H = hist[lane];
-        uint32_t pre = H;   // inclusive prefix sum over lanes: #{e <= lane}
-#pragma unroll
-        for (uint32_t o = 1; o < 64u; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)pre, o);
-            if (lane >= o) pre += y;
-        }
-        const uint32_t nn_l = spp - pre;   // n_{k+1} for k = lane
+        const uint32_t H = hist[lane];   // lane k: #{e == k} over the pixel (pass 1)
+        const uint32_t nn_l = spp - wave_scan_dpp(H);   // n_{k+1} = #{e > k} for k = lane
         uint32_t cge = 0, ceq = 0;   // lane k: samples of the earlier chunks with e >= k, e == k
+        // Per chunk, each retiring lane needs #{lanes below with e' >= e} and #{... e' == e}.  With the
+        // values clamped to ec = min(e, K) (nb bits; survivors and e >= K compare as K), the wave
+        // ballots ec's bit planes once per chunk and every lane compares itself against all lanes at
+        // once, most significant bit first: gt collects the lanes found greater, eq those still equal.
+        // Round 2 ran one pass per distinct bounce in the chunk (ballots, readlanes and selects each).
+        const uint32_t nb = 32u - (uint32_t)__builtin_clz(K);   // ec in [0, K], K <= 64: 1..7 bits
+#ifdef RT_EXP_DUP_REPLAY   // timing experiment: the replay twice (the same map writes)
+        for (uint32_t rep = 0; rep < 2u; ++rep) {
+            asm volatile("" ::: "memory");
+            cge = 0; ceq = 0;
+#endif
         for (uint32_t b = 0; b < spp; b += 512u) {   // the samples in order, 64 at a time
             uint32_t ev[8];
 #pragma unroll
@@ -1802,27 +1820,36 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 if (b + 64u * u >= spp) break;
                 const uint32_t i = b + 64u * u + lane, e = ev[u];
                 const bool in = i < spp, ret = e < K;
-                unsigned long long rem = __ballot(ret);
-                uint32_t pold = 0, pnew = 0, hc = 0, gadd = 0, nn = 0;
-                while (rem != 0ull) {   // one pass per distinct bounce k among the chunk's retiring lanes
-                    const uint32_t k = __builtin_amdgcn_readlane(e, (int)__builtin_ctzll(rem));
-                    const unsigned long long bge = __ballot(in && e >= k), beq = __ballot(e == k);
-                    const uint32_t cnt = (uint32_t)__popcll(beq);
-                    const uint32_t cg = __builtin_amdgcn_readlane(cge, (int)k), cq = __builtin_amdgcn_readlane(ceq, (int)k);
-                    const uint32_t n1 = __builtin_amdgcn_readlane(nn_l, (int)k);
-                    if (e == k) {
-                        pold = cg + (uint32_t)__popcll(bge & lt_mask);
-                        pnew = n1 + cq + (uint32_t)__popcll(beq & lt_mask);
-                        nn = n1;
-                    }
-                    if (lane <= k) gadd += cnt;   // lane j: this chunk's #{e >= j}
-                    if (lane == k) hc = cnt;
-                    rem &= ~beq;
+                const uint32_t ec = ret ? e : K;
+                const unsigned long long inm = __ballot(in);
+                // eq, gt: the lanes equal to / greater than this lane's ec; eqk: the lanes whose ec equals
+                // this lane's index k (lane k's count of e == k).  A plane no lane sets changes neither eq
+                // nor gt, and clears eqk in the lanes k with that bit (zb)
+                unsigned long long eq = inm, gt = 0ull, eqk = inm;
+                uint32_t zb = 0;
+                for (uint32_t bb = nb; bb-- > 0u;) {
+                    const unsigned long long P = __ballot(in && ((ec >> bb) & 1u));
+                    if (P == 0ull) { zb |= 1u << bb; continue; }
+                    const unsigned long long B = ((ec >> bb) & 1u) ? ~0ull : 0ull;     // this lane's bit
+                    const unsigned long long Bk = ((lane >> bb) & 1u) ? ~0ull : 0ull;  // bit of k = lane
+                    gt |= eq & P & ~B;     // equal so far, 1 where this lane has 0: greater
+                    eq &= ~(P ^ B);        // still equal
+                    eqk &= ~(P ^ Bk);
                 }
-                cge += gadd + (uint32_t)__popcll(__ballot(in && e >= K));
-                ceq += hc;
                 const uint32_t ek = ret ? e : 0u;
+                // the earlier chunks' counts at this lane's bounce
+                const uint32_t cg = (uint32_t)__shfl((int)cge, (int)ek), cq = (uint32_t)__shfl((int)ceq, (int)ek);
+                const uint32_t nn = (uint32_t)__shfl((int)nn_l, (int)ek);
+                // lane k < K: #{e == k} in this chunk (lanes k >= 2^nb or > K are never read)
+                const uint32_t h = (lane & zb) != 0u ? 0u : (uint32_t)__popcll(eqk);
+                // lane k <= K: #{in && e >= k} = #{in} - #{e < k}
+                cge += (uint32_t)__popcll(inm) - (wave_scan_dpp(h) - h);
+                ceq += h;
                 if (ret) {
+                    // Sample i, terminated at bounce e, sat at pold = #{s' < i : e_s' >= e} during bounce e
+                    // and moves to pnew = n_{e+1} + #{s' < i : e_s' == e}
+                    const uint32_t pold = cg + (uint32_t)__popcll((gt | eq) & lt_mask);
+                    const uint32_t pnew = nn + cq + (uint32_t)__popcll(eq & lt_mask);
                     const uint32_t Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
                     // positions [lo, 4 ceil(n_k / 4)) retire at bounce e; pold and pnew are below n_k <= 4 Lk (pold
                     // counts the earlier samples with e >= k, pnew = n_{k+1} + the earlier ones with
@@ -1837,6 +1864,9 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 }
             }
         }
+#ifdef RT_EXP_DUP_REPLAY
+        }
+#endif
     }
 #endif
     // vectorized3 (ray_tracing.rs:508-628): replay the in-place swap partitions.  After bounce k the
@@ -1977,6 +2007,10 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         // the 12 running sums live in LDS (the free histogram) between batches: a short live range
         // keeps this loop from raising the kernel's register peak
         T* accl = (T*)hist;
+#ifdef RT_EXP_DUP_REDUCE   // timing experiment: the final reduction twice (the same sums)
+        for (uint32_t rep = 0; rep < 2u; ++rep) {
+            asm volatile("" ::: "memory");
+#endif
         if (lane < 12u) accl[lane] = T(0.0);
         for (uint32_t qb = 0; qb < P; qb += 64u) {
             const uint32_t qq = qb + lane;
@@ -2041,6 +2075,9 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
             }
             __builtin_amdgcn_wave_barrier();
         }
+#ifdef RT_EXP_DUP_REDUCE
+        }
+#endif
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane < 12u) acc = accl[lane];
     }
@@ -2312,15 +2349,6 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         T bt = T(0);
         int bi = -1;
 #ifndef RT_EXP_NO_CAMCULL
-#ifdef RT_EXP_DUP_CAM   // timing experiment: the camera sweep twice (same result)
-        {
-            V3<T> bd2 = bd;
-            asm volatile("" : "+v"(bd2.x));
-            T bt2;
-            const int bi2 = camera_sweep<T, ROOT2, SC, MEGA>(v, bd2, bt2);
-            asm volatile("" ::"v"(bi2), "v"(bt2));
-        }
-#endif
         {
             // the batch's pixel slots (one, or two where a pixel's samples end inside the batch)
             uint32_t smask = 0;
@@ -2339,12 +2367,25 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                     need &= need - 1u;
                     const uint32_t pxi = __builtin_amdgcn_readfirstlane(s_slotpix[wave][sl]);
                     const uint32_t row = pxi / iw;
+#ifdef RT_EXP_DUP_PLIST   // timing experiment: each pixel's candidate list built twice (same list)
+                    { uint32_t r2 = row; asm volatile("" : "+s"(r2)); (void)pixel_list<T, MEGA>(pxi - r2 * iw, r2, s_clist[wave][sl]); }
+#endif
                     (void)pixel_list<T, MEGA>(pxi - row * iw, row, s_clist[wave][sl]);
                 }
             }
             bool listed = true;
             for (uint32_t m = smask; m != 0u; m &= m - 1u)
                 if (__builtin_amdgcn_readfirstlane(s_clist[wave][__builtin_ctz(m)][0]) == 0xFFFFu) listed = false;
+#ifdef RT_EXP_DUP_CAM   // timing experiment: the batch's camera stage (listed or swept) twice (same result)
+            {
+                V3<T> bd2 = bd;
+                asm volatile("" : "+v"(bd2.x));
+                T bt2;
+                const int bi2 = listed ? camera_listed<T, ROOT2, SC>(v, bd2, bt2, s_clist[wave], smask)
+                                       : camera_sweep<T, ROOT2, SC, MEGA>(v, bd2, bt2);
+                asm volatile("" ::"v"(bi2), "v"(bt2));
+            }
+#endif
             if (listed) bi = camera_listed<T, ROOT2, SC>(v, bd, bt, s_clist[wave], smask);
             else bi = camera_sweep<T, ROOT2, SC, MEGA>(v, bd, bt);   // whole wave: lanes are spheres in the cull
         }
