@@ -2837,14 +2837,20 @@ static SweepLayout build_layout(const rt_scene* s) {
     L.n_xs = (uint32_t)exact.size();
     while (L.slot.size() % 4) L.slot.push_back(-1);
     L.n_xg = (uint32_t)(L.slot.size() / 4);
-    // k-d split; the left part takes a multiple of kClusterMax so that leaves stay full
-    std::vector<std::pair<size_t, size_t>> work{{0, filt.size()}};
-    while (!work.empty()) {
-        const auto [b, e] = work.back();
-        work.pop_back();
-        if (e - b <= kClusterMax) {
+    // k-d split (median along the longest extent of the centres), aligned to the box hierarchy above
+    // the clusters: a node of more than 256 spheres (4 supers = one mega) gives its left part a
+    // multiple of 256, a node of 65..256 a multiple of 64 (one super), smaller nodes a multiple of 16,
+    // and each child's clusters are padded with empty ones to a whole number of its parent's unit
+    // (the next sibling then starts on a super / mega boundary).  So every super box and mega box
+    // bounds one k-d subtree.  Round 2 split at multiples of 16 only:
+    // at config E (10 000 spheres, a 313-cluster left half) every super and mega on the right of a
+    // split took clusters of two subtrees, and their boxes spanned both.
+    auto build = [&](auto&& self, size_t b, size_t e, size_t pad) -> void {   // pad: clusters per block
+        const size_t N = e - b, c0 = L.members.size();
+        if (N <= kClusterMax) {
             if (e > b) L.members.emplace_back(filt.begin() + b, filt.begin() + e);
-            continue;
+            while ((L.members.size() - c0) % pad) L.members.emplace_back();
+            return;
         }
         double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
         for (size_t k = b; k < e; ++k)
@@ -2854,14 +2860,17 @@ static SweepLayout build_layout(const rt_scene* s) {
             }
         int ax = 0;
         for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
-        const size_t m = b + std::min(e - b - 1, (e - b + 2 * kClusterMax - 1) / (2 * kClusterMax) * kClusterMax);
+        const size_t unit = N > 16 * kClusterMax ? 16 * kClusterMax : N > 4 * kClusterMax ? 4 * kClusterMax : kClusterMax;
+        const size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
         std::nth_element(filt.begin() + b, filt.begin() + m, filt.begin() + e, [&](uint32_t x, uint32_t y) {
             const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
             return cx < cy || (cx == cy && x < y);
         });
-        work.push_back({m, e});
-        work.push_back({b, m});
-    }
+        self(self, b, m, unit / kClusterMax);
+        self(self, m, e, unit / kClusterMax);
+        while ((L.members.size() - c0) % pad) L.members.emplace_back();
+    };
+    build(build, 0, filt.size(), 1);
     while (L.members.size() % 4) L.members.emplace_back();
     for (auto& c : L.members) {
         std::sort(c.begin(), c.end());

@@ -504,19 +504,20 @@ def test_one_context_two_streams(renderer, scene_100):
             hip.hipStreamDestroy(st)
 
 
-@pytest.mark.parametrize("depth", [60, 200])
+@pytest.mark.parametrize("depth", [60, 63, 64, 65, 200])
 @pytest.mark.parametrize("prec", [0, abi.RT_FLAG_F32])
 def test_long_paths_replay(renderer, depth, prec):
     """Camera inside a glass sphere, 38 units off its centre, with root2 allowed: rays that meet
     the glass beyond the critical angle are trapped by total internal reflection for all `depth`
     bounces, others escape after a few.  Measured per-pixel K (bounce-loop iterations) at depth
     200: 77 pixels at 2-4, 67 at 200, so the position replay in finish_pixel runs far past 64
-    bounces, with long and short paths mixed in one wave."""
+    bounces, with long and short paths mixed in one wave.  Depths 63 and 64 take the bit-plane replay
+    to its widest comparisons (K = 63: 6 planes, K = 64: 7), 65 the per-bounce loop for K > 64."""
     flat = rt.FlatScene(np.array([[16.0, 2.0, 56.5]]), np.array([40.0]), np.array([0], np.uint32),
                         [rt.Dielectric(1.5, False)])
     lin, st = assert_parity(renderer, flat, cam_for(16, 9), depth, 24, abi.RT_FLAG_ROOT2 | prec)
     # bounce_iters sums each pixel's K = min(depth, longest path + 1); measured: 4224 at depth 60
-    assert st.bounce_iters > 9 * 16 * (20 if depth < 64 else 40)
+    assert st.bounce_iters > 9 * 16 * (20 if depth < 100 else 40)
 
 
 # ---- general-sweep distance filter (nearest_hit / filter_group): never changes a result ----
