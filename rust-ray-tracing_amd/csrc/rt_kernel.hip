@@ -62,7 +62,7 @@
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
                             defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
                             defined(RT_EXP_DUP_MEGABOX) || defined(RT_EXP_DUP_PLIST) || defined(RT_EXP_DUP_REPLAY) || \
-                            defined(RT_EXP_DUP_REDUCE) || \
+                            defined(RT_EXP_DUP_REDUCE) || defined(RT_EXP_SAH) || \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -2802,13 +2802,16 @@ static void pack_filter(const std::vector<T>& cen, uint32_t n, std::vector<float
 
 // Spatial clusters for the general sweep's two-level filter (nearest_hit).  Slot order: first the
 // "always exact" spheres (pack_filter's rule: non-finite, or |c|_1 + r above 8x the median, e.g. a
-// ground sphere) in scene order, padded to whole groups -- every ray tests them exactly; then the
+// ground sphere; and up to kBigExact spheres of more than kBigRatio x the median radius) in scene
+// order, padded to whole groups -- every ray tests them exactly; then the
 // filterable spheres, split k-d style (median along the longest extent of the centres) into
 // clusters of at most kClusterMax = 16 spheres, each cluster in 4 whole groups (dummy-padded).  The
 // cluster count is padded to whole top groups of 4 with empty clusters (never taken).  The sweep
 // visits spheres in slot order, not scene order: hit_update's tie rule (equal t -> the later scene
 // index wins; scalar mode: the earlier) makes the nearest hit independent of the visiting order.
 constexpr uint32_t kClusterMax = 16;
+constexpr double kBigRatio = 3.0;   // "big": radius above 3x the median radius of the filtered spheres
+constexpr size_t kBigExact = 8;     // at most this many big spheres join the always-exact ones
 struct SweepLayout {
     std::vector<int32_t> slot;                   // slot -> scene index, -1 = dummy (4 slots per group)
     std::vector<std::vector<uint32_t>> members;  // per cluster (count padded to a multiple of 4)
@@ -2831,6 +2834,26 @@ static SweepLayout build_layout(const rt_scene* s) {
     for (uint32_t i = 0; i < n; ++i) {
         const bool fin = std::isfinite(key[i]) && std::isfinite(s->radius[i] * s->radius[i]);
         (fin && !(key[i] > kExactRatio * median) ? filt : exact).push_back(i);
+    }
+    // A few spheres far larger than the typical one (RTIOW's three radius-1 spheres among radius-0.2
+    // ones) are tested exactly by every ray too: in a cluster, one of them made its box 5x taller, and
+    // every ray passing over the small spheres near it walked the cluster.  At most kBigExact of them
+    // (more stay in clusters: exact tests for every ray would cost more).  Same-box C fp32 +5.1 %,
+    // B +4.1 %, E +3.1 % (profiles/r03/experiments/big_exact.txt).
+    {
+        std::vector<double> rr;
+        for (uint32_t i : filt) rr.push_back(std::fabs(s->radius[i]));
+        if (!rr.empty()) {
+            std::nth_element(rr.begin(), rr.begin() + rr.size() / 2, rr.end());
+            const double mr = rr[rr.size() / 2];
+            std::vector<uint32_t> keep, big;
+            for (uint32_t i : filt) (std::fabs(s->radius[i]) > kBigRatio * mr ? big : keep).push_back(i);
+            if (!big.empty() && big.size() <= kBigExact) {
+                filt.swap(keep);
+                exact.insert(exact.end(), big.begin(), big.end());
+                std::sort(exact.begin(), exact.end());
+            }
+        }
     }
     SweepLayout L;
     for (uint32_t i : exact) L.slot.push_back((int32_t)i);
@@ -2861,7 +2884,44 @@ static SweepLayout build_layout(const rt_scene* s) {
         int ax = 0;
         for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
         const size_t unit = N > 16 * kClusterMax ? 16 * kClusterMax : N > 4 * kClusterMax ? 4 * kClusterMax : kClusterMax;
-        const size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
+        size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
+#ifdef RT_EXP_SAH   // split axis and position (multiples of unit) by the surface-area heuristic
+        {
+            double best = INFINITY;
+            int bax = ax;
+            size_t bm = m;
+            std::vector<uint32_t> ord(filt.begin() + b, filt.begin() + e);
+            std::vector<double> sl(N + 1), sr(N + 1);
+            for (int a = 0; a < 3; ++a) {
+                std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+                    const double cx = s->center[3 * x + a], cy = s->center[3 * y + a];
+                    return cx < cy || (cx == cy && x < y);
+                });
+                auto sweep = [&](bool fwd, std::vector<double>& out) {
+                    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+                    out[fwd ? 0 : N] = 0.0;
+                    for (size_t k = 0; k < N; ++k) {
+                        const uint32_t i = ord[fwd ? k : N - 1 - k];
+                        const double r = std::fabs(s->radius[i]);
+                        for (int q = 0; q < 3; ++q) {
+                            lo[q] = std::min(lo[q], s->center[3 * i + q] - r);
+                            hi[q] = std::max(hi[q], s->center[3 * i + q] + r);
+                        }
+                        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+                        out[fwd ? k + 1 : N - 1 - k] = dx * dy + dy * dz + dz * dx;
+                    }
+                };
+                sweep(true, sl);
+                sweep(false, sr);
+                for (size_t k = unit; k < N; k += unit) {
+                    const double cst = sl[k] * (double)k + sr[k] * (double)(N - k);
+                    if (cst < best) { best = cst; bax = a; bm = b + k; }
+                }
+            }
+            ax = bax;
+            m = bm;
+        }
+#endif
         std::nth_element(filt.begin() + b, filt.begin() + m, filt.begin() + e, [&](uint32_t x, uint32_t y) {
             const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
             return cx < cy || (cx == cy && x < y);
