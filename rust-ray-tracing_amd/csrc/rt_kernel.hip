@@ -62,7 +62,7 @@
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_LMAP_CAP) ||   \
                             defined(RT_EXP_DUP_CLBOX) || defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) ||  \
                             defined(RT_EXP_DUP_MEGABOX) || defined(RT_EXP_DUP_PLIST) || defined(RT_EXP_DUP_REPLAY) || \
-                            defined(RT_EXP_DUP_REDUCE) || defined(RT_EXP_SAH) || \
+                            defined(RT_EXP_DUP_REDUCE) || \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif
@@ -2884,44 +2884,7 @@ static SweepLayout build_layout(const rt_scene* s) {
         int ax = 0;
         for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
         const size_t unit = N > 16 * kClusterMax ? 16 * kClusterMax : N > 4 * kClusterMax ? 4 * kClusterMax : kClusterMax;
-        size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
-#ifdef RT_EXP_SAH   // split axis and position (multiples of unit) by the surface-area heuristic
-        {
-            double best = INFINITY;
-            int bax = ax;
-            size_t bm = m;
-            std::vector<uint32_t> ord(filt.begin() + b, filt.begin() + e);
-            std::vector<double> sl(N + 1), sr(N + 1);
-            for (int a = 0; a < 3; ++a) {
-                std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
-                    const double cx = s->center[3 * x + a], cy = s->center[3 * y + a];
-                    return cx < cy || (cx == cy && x < y);
-                });
-                auto sweep = [&](bool fwd, std::vector<double>& out) {
-                    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-                    out[fwd ? 0 : N] = 0.0;
-                    for (size_t k = 0; k < N; ++k) {
-                        const uint32_t i = ord[fwd ? k : N - 1 - k];
-                        const double r = std::fabs(s->radius[i]);
-                        for (int q = 0; q < 3; ++q) {
-                            lo[q] = std::min(lo[q], s->center[3 * i + q] - r);
-                            hi[q] = std::max(hi[q], s->center[3 * i + q] + r);
-                        }
-                        const double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
-                        out[fwd ? k + 1 : N - 1 - k] = dx * dy + dy * dz + dz * dx;
-                    }
-                };
-                sweep(true, sl);
-                sweep(false, sr);
-                for (size_t k = unit; k < N; k += unit) {
-                    const double cst = sl[k] * (double)k + sr[k] * (double)(N - k);
-                    if (cst < best) { best = cst; bax = a; bm = b + k; }
-                }
-            }
-            ax = bax;
-            m = bm;
-        }
-#endif
+        const size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
         std::nth_element(filt.begin() + b, filt.begin() + m, filt.begin() + e, [&](uint32_t x, uint32_t y) {
             const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
             return cx < cy || (cx == cy && x < y);
