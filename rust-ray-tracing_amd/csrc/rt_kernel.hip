@@ -2895,8 +2895,32 @@ static SweepLayout build_layout(const rt_scene* s) {
     };
     build(build, 0, filt.size(), 1);
     while (L.members.size() % 4) L.members.emplace_back();
+    // Members ordered by k-d halving (16 -> 8|8 -> 4|4 -> 2|2), so each filter group and each exact pair
+    // holds neighbours: a lane's passes concentrate in fewer groups and pairs.  Scene-index order (round
+    // 2) grouped spheres along the generator's loop.  Same-box C fp32 +0.5 %, fp64 +0.7 %, E +0.4 %.
+    auto kd_order = [&](auto&& self, std::vector<uint32_t>& v, size_t b, size_t e) -> void {
+        if (e - b <= 2) return;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (size_t k = b; k < e; ++k)
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], s->center[3 * v[k] + a]);
+                hi[a] = std::max(hi[a], s->center[3 * v[k] + a]);
+            }
+        int ax = 0;
+        for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
+        size_t half = 1;
+        while (2 * half < e - b) half *= 2;   // power-of-two left part: groups of 4 stay whole
+        const size_t m = b + half;
+        std::nth_element(v.begin() + b, v.begin() + m, v.begin() + e, [&](uint32_t x, uint32_t y) {
+            const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
+            return cx < cy || (cx == cy && x < y);
+        });
+        self(self, v, b, m);
+        self(self, v, m, e);
+    };
     for (auto& c : L.members) {
         std::sort(c.begin(), c.end());
+        kd_order(kd_order, c, 0, c.size());
         for (uint32_t k = 0; k < kClusterMax; ++k) L.slot.push_back(k < c.size() ? (int32_t)c[k] : -1);
     }
     return L;
