@@ -173,6 +173,8 @@ template <typename T> struct KParams {
     const float* lclb;         // ... the box levels in group-local frames (pack_local_boxes): per super its
     const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
     const float* lmeg;
+    const float* lgig;         //     and per giga group its 4 gigas (a giga: one mega group, 4 megas)
+    uint32_t n_gg;             // giga groups (0: the megas are tested without the giga pre-test)
     float l_r2max, l_hir2, l_isr;   // their margin constants: max local r2f, 48 u 0.5 / min, 8 u / sqrt(min)
     // ... and the mega walk's order (<= 64 megas): a grid over the megas' union, per cell 4 u64 words
     // {touching, within 1/4 of a mega's size, within 1/2, 0} (pack_mega_tiers)
@@ -1028,15 +1030,33 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
 #pragma unroll 1
                 for (uint32_t k = 0; k < 3u; ++k) {
                     if (k == kTest) {
-                        n_box += nt;
-                        for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
-                            lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
-                                KSTAT(5);
+                        const uint32_t ngg = span == 16u ? qa.n_gg : 0u;
+                        if (ngg != 0u) {
+                            // Gigas (one mega group's 4 megas each, k-d subtrees): the giga boxes first, then
+                            // the mega groups of the passing gigas only.  A giga box holds its megas' boxes,
+                            // so a mega of a culled giga would fail its own test: tm is unchanged.
+                            uint32_t gm = 0;
+                            n_box += ngg;
+                            lbox_loop((cptr<float>)__builtin_assume_aligned(qa.lgig, 64), ngg,
+                                      [&](const LBoxGroup& cur, uint32_t t) { gm |= lmask(cur) << (4u * t); });
+                            gm &= (1u << nt) - 1u;
+                            while (gm != 0u) {
+                                const uint32_t gg = (uint32_t)__builtin_ctz(gm);
+                                gm &= gm - 1u;
+                                ++n_box;
+                                tm |= (uint64_t)lmask(load_lbox(lm, gg)) << (4u * gg);
+                            }
+                        } else {
+                            n_box += nt;
+                            for (uint32_t t1 = 0; t1 < nt; t1 += 8u)
+                                lbox_loop(lm + 32u * (t0 + t1), min(8u, nt - t1), [&](const LBoxGroup& cur, uint32_t t) {
+                                    KSTAT(5);
 #ifdef RT_EXP_DUP_MEGABOX   // timing experiment: the mega-box tests twice (same result)
-                                { LBoxGroup c2 = cur; asm volatile("" : "+s"(c2.v[0])); const uint32_t m2 = lmask(c2); asm volatile("" :: "s"(m2)); }
+                                    { LBoxGroup c2 = cur; asm volatile("" : "+s"(c2.v[0])); const uint32_t m2 = lmask(c2); asm volatile("" :: "s"(m2)); }
 #endif
-                                tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
-                            });
+                                    tm |= (uint64_t)lmask(cur) << (4u * (t1 + t));
+                                });
+                        }
                         tm &= valid;
                     }
                     uint64_t w = k == 0u ? (kTest == 0u ? tm & T0 : T0)
@@ -2559,7 +2579,8 @@ struct rt_context {
     void* meg64 = nullptr; void* meg32 = nullptr;   // mega boxes (4 supers each; big scenes only)
     void* lfs64 = nullptr; void* lfs32 = nullptr;   // cluster-local filter groups (big scenes only)
     void* lcl64 = nullptr; void* lcl32 = nullptr;   // ... and the per-cluster frame records
-    void* lbx64[3] = {}; void* lbx32[3] = {};       // local box levels: cluster boxes, supers, megas
+    void* lbx64[4] = {}; void* lbx32[4] = {};       // local box levels: cluster boxes, supers, megas, gigas
+    uint32_t n_gg = 0;
     float l_r2max64 = 0, l_r2min64 = 0, l_r2max32 = 0, l_r2min32 = 0;
     uint32_t n_mg = 0;
     void* mtiers = nullptr;                         // the mega walk's order table (pack_mega_tiers)
@@ -2664,12 +2685,13 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->meg64); (void)hipFree(c->meg32);
     (void)hipFree(c->lfs64); (void)hipFree(c->lfs32); (void)hipFree(c->lcl64); (void)hipFree(c->lcl32);
     c->lfs64 = c->lfs32 = c->lcl64 = c->lcl32 = nullptr;
-    for (int lv = 0; lv < 3; ++lv) {
+    for (int lv = 0; lv < 4; ++lv) {
         (void)hipFree(c->lbx64[lv]); (void)hipFree(c->lbx32[lv]);
         c->lbx64[lv] = c->lbx32[lv] = nullptr;
     }
     c->meg64 = c->meg32 = nullptr;
     c->n_mg = 0;
+    c->n_gg = 0;
     (void)hipFree(c->mtiers);
     c->mtiers = nullptr;
     (void)hipFree(c->clus64); (void)hipFree(c->clus32); (void)hipFree(c->cullc64); (void)hipFree(c->cullc32);
@@ -2817,6 +2839,7 @@ struct SweepLayout {
     std::vector<std::vector<uint32_t>> members;  // per cluster (count padded to a multiple of 4)
     uint32_t n_xg = 0;                           // leading groups of always-exact spheres
     uint32_t n_xs = 0;                           // always-exact spheres (slots 0 .. n_xs-1)
+    bool giga = false;                           // splits aligned to gigas (1024 spheres) as well
 };
 static SweepLayout build_layout(const rt_scene* s) {
     const uint32_t n = s->n_spheres;
@@ -2883,7 +2906,8 @@ static SweepLayout build_layout(const rt_scene* s) {
             }
         int ax = 0;
         for (int a = 1; a < 3; ++a) if (hi[a] - lo[a] > hi[ax] - lo[ax]) ax = a;
-        const size_t unit = N > 16 * kClusterMax ? 16 * kClusterMax : N > 4 * kClusterMax ? 4 * kClusterMax : kClusterMax;
+        const size_t unit = L.giga && N > 64 * kClusterMax ? 64 * kClusterMax : N > 16 * kClusterMax ? 16 * kClusterMax
+                          : N > 4 * kClusterMax ? 4 * kClusterMax : kClusterMax;
         const size_t m = b + std::min(N - 1, (N + 2 * unit - 1) / (2 * unit) * unit);
         std::nth_element(filt.begin() + b, filt.begin() + m, filt.begin() + e, [&](uint32_t x, uint32_t y) {
             const double cx = s->center[3 * x + ax], cy = s->center[3 * y + ax];
@@ -2893,6 +2917,7 @@ static SweepLayout build_layout(const rt_scene* s) {
         self(self, m, e, unit / kClusterMax);
         while ((L.members.size() - c0) % pad) L.members.emplace_back();
     };
+    L.giga = filt.size() > 128 * kClusterMax;   // the mega kernels' scenes (more than 8 super groups)
     build(build, 0, filt.size(), 1);
     while (L.members.size() % 4) L.members.emplace_back();
     // Members ordered by k-d halving (16 -> 8|8 -> 4|4 -> 2|2), so each filter group and each exact pair
@@ -3098,7 +3123,7 @@ constexpr uint32_t kLBoxFloats = 32;
 template <typename T>
 static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, const std::vector<float>& r2l,
                              std::vector<float>& lclb, std::vector<float>& lsup, std::vector<float>& lmeg,
-                             float& r2max, float& r2min, std::vector<float>* wmeg = nullptr) {
+                             std::vector<float>& lgig, float& r2max, float& r2min, std::vector<float>* wmeg = nullptr) {
     auto up32 = [](double v) -> float {
         float f = (float)v;
         if ((double)f < v) f = std::nextafter(f, std::numeric_limits<float>::infinity());
@@ -3217,6 +3242,12 @@ static void pack_local_boxes(const std::vector<T>& cen, const SweepLayout& L, co
     localise(wcl, (nc + 3) / 4, lclb);
     localise(wsu, nsg, lsup);
     localise(wme, (nsg + 3) / 4, lmeg);
+    // gigas: the union of each mega group's 4 megas (build_layout aligns them to k-d subtrees in scenes
+    // of more than 2048 filtered spheres)
+    const size_t nmg = (nsg + 3) / 4;
+    std::vector<float> wgi;
+    unite(wme, nmg, wgi);
+    localise(wgi, (nmg + 3) / 4, lgig);
 }
 
 // The mega walk's order table (nearest_hit, MEGA): a grid of cubic cells (<= 4096, <= 64 per axis)
@@ -3332,17 +3363,18 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
             std::vector<float> lf64, lf32, lr64, lr32, q64, q32;
             pack_local(c64, L, t64, lf64, lr64, q64);
             pack_local(c32, L, t32, lf32, lr32, q32);
-            std::vector<float> b64[3], b32[3];
-            pack_local_boxes(c64, L, q64, b64[0], b64[1], b64[2], c->l_r2max64, c->l_r2min64);
+            std::vector<float> b64[4], b32[4];
+            pack_local_boxes(c64, L, q64, b64[0], b64[1], b64[2], b64[3], c->l_r2max64, c->l_r2min64);
             std::vector<float> wme;
-            pack_local_boxes(c32, L, q32, b32[0], b32[1], b32[2], c->l_r2max32, c->l_r2min32, &wme);
+            pack_local_boxes(c32, L, q32, b32[0], b32[1], b32[2], b32[3], c->l_r2max32, c->l_r2min32, &wme);
+            c->n_gg = L.giga && c->n_mg <= 16u ? (c->n_mg + 3u) / 4u : 0u;
             {
                 const MegaTiers M = pack_mega_tiers(wme, (L.members.size() / 4 + 3) / 4);
                 if ((rc = up(&c->mtiers, M.t.data(), M.t.size() * sizeof(uint64_t))) != RT_OK) return rc;
                 for (int a = 0; a < 3; ++a) { c->mt_lo[a] = M.lo[a]; c->mt_n[a] = M.n[a]; }
                 c->mt_inv = M.inv;
             }
-            for (int lv = 0; lv < 3; ++lv) {
+            for (int lv = 0; lv < 4; ++lv) {
                 if ((rc = up(&c->lbx64[lv], b64[lv].data(), b64[lv].size() * sizeof(float))) != RT_OK) return rc;
                 if ((rc = up(&c->lbx32[lv], b32[lv].data(), b32[lv].size() * sizeof(float))) != RT_OK) return rc;
             }
@@ -3513,6 +3545,8 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.lclb = (const float*)(f64 ? c->lbx64[0] : c->lbx32[0]);
     p.lsup = (const float*)(f64 ? c->lbx64[1] : c->lbx32[1]);
     p.lmeg = (const float*)(f64 ? c->lbx64[2] : c->lbx32[2]);
+    p.lgig = (const float*)(f64 ? c->lbx64[3] : c->lbx32[3]);
+    p.n_gg = c->n_gg;
     p.mtiers = (const uint64_t*)c->mtiers;
     for (int a = 0; a < 3; ++a) { p.mt_lo[a] = c->mt_lo[a]; p.mt_n[a] = c->mt_n[a]; }
     p.mt_inv = c->mt_inv;
