@@ -2862,7 +2862,7 @@ static SweepLayout build_layout(const rt_scene* s) {
     // ones) are tested exactly by every ray too: in a cluster, one of them made its box 5x taller, and
     // every ray passing over the small spheres near it walked the cluster.  At most kBigExact of them
     // (more stay in clusters: exact tests for every ray would cost more).  Same-box C fp32 +5.1 %,
-    // B +4.1 %, E +3.1 % (profiles/r03/experiments/big_exact.txt).
+    // fp64 +5.4 %, B +4.1 %, E +3.1 % (profiles/r03/experiments/big_exact.txt).
     {
         std::vector<double> rr;
         for (uint32_t i : filt) rr.push_back(std::fabs(s->radius[i]));
