@@ -355,6 +355,18 @@ def test_mega_walk_shapes(renderer, flags, n):
     assert_parity(renderer, flat, cam_for(4, 3), 50, 32, flags)
 
 
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_F32, 0])
+@pytest.mark.parametrize("n", [20, 261, 1029, 2053, 2600, 4100])
+def test_layout_padding_shapes(renderer, flags, n):
+    """The hierarchy-aligned layout (build_layout) at sphere counts just past its units: 16-sphere
+    clusters, 64 (supers), 256 (megas) and 1024 (gigas, scenes over 2048 filtered spheres), so
+    children are padded with empty clusters in the middle of the streams; and the big spheres in
+    the always-exact group.  Against the oracle in both precisions."""
+    flat = rt.scenes.random_spheres(n).flatten()
+    assert flat.n_spheres == n
+    assert_parity(renderer, flat, cam_for(8, 5), 50, 16, flags)
+
+
 # ---- semantics modes (tests/test_modes.py pins them on the CPU) ----
 MODES = [abi.RT_FLAG_MODE_VECTORIZED, abi.RT_FLAG_MODE_VECTORIZED | abi.RT_FLAG_ROOT2, abi.RT_FLAG_MODE_SCALAR,
          abi.RT_FLAG_MODE_VECTORIZED3, abi.RT_FLAG_MODE_VECTORIZED3 | abi.RT_FLAG_ROOT2]
