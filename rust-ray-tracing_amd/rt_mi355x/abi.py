@@ -96,9 +96,17 @@ EXPORTED = [
 
 _lib = None
 
-# The sources the Makefile hashes into rt_version() ("src=<hash>"), in its order.
-SOURCE_FILES = [os.path.join(PKG_DIR, "csrc", "rt_kernel.hip"), os.path.join(PKG_DIR, "csrc", "rt_device.hpp"),
-                os.path.join(os.path.dirname(PKG_DIR), "include", "rt_mi355x.h")]
+# The sources the Makefile hashes into rt_version() ("src=<hash>"), in its order (SRC, then HDR).
+KERNEL_SOURCES = ["rt_kernel.hip", "rt_experiments.hpp", "rt_common.hpp", "rt_sweep.hpp", "rt_camera.hpp",
+                  "rt_finish.hpp", "rt_trace.hpp", "rt_layout.hpp", "rt_device.hpp"]
+SOURCE_FILES = [os.path.join(PKG_DIR, "csrc", f) for f in KERNEL_SOURCES] + \
+               [os.path.join(os.path.dirname(PKG_DIR), "include", "rt_mi355x.h")]
+
+
+def kernel_source_text():
+    """The text of every csrc/ file (the one translation unit the library is built from), concatenated:
+    tests that pin a constant or a margin formula of the kernel search this."""
+    return "\n".join(open(f).read() for f in SOURCE_FILES[:-1])
 
 
 def source_hash():

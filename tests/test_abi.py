@@ -133,8 +133,18 @@ def test_header_constants_match_python_mirror():
 
 
 # ---- build kinds (product vs experiment) and the source hash -------------------------------------
-KERNEL = os.path.join(REPO, "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")
+CSRC = os.path.join(REPO, "rust-ray-tracing_amd", "csrc")
+EXPERIMENTS = os.path.join(CSRC, "rt_experiments.hpp")
+EXP_PATCHES = os.path.join(REPO, "tools", "exp")
 MAKEFILE = os.path.join(REPO, "rust-ray-tracing_amd", "Makefile")
+
+
+def _csrc_files():
+    return sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".hpp")))
+
+
+def _patches():
+    return sorted(os.path.join(EXP_PATCHES, f) for f in os.listdir(EXP_PATCHES) if f.endswith(".patch"))
 
 
 def test_product_library_reports_its_sources():
@@ -147,20 +157,49 @@ def test_product_library_reports_its_sources():
     assert v["src_hash"] == abi.source_hash(), (v, "rebuild: make -C rust-ray-tracing_amd")
 
 
+def test_every_source_is_hashed():
+    """Every csrc/ file is in the source hash (abi.SOURCE_FILES, the Makefile's SRC + HDR)."""
+    hashed = {os.path.basename(f) for f in abi.SOURCE_FILES}
+    assert set(_csrc_files()) <= hashed, sorted(set(_csrc_files()) - hashed)
+    mk = open(MAKEFILE).read()
+    for f in _csrc_files():
+        assert "csrc/" + f in mk, f
+
+
 def test_every_experiment_macro_is_refused_by_the_product_build():
-    """Each RT_EXP_* (and RT_KSTATS) macro the kernel tests is in the #error list the product build
-    (-DRT_PRODUCT) checks, and the product rule defines RT_PRODUCT and no experiment macro."""
-    src = open(KERNEL).read()
+    """Each RT_EXP_* (and RT_KSTATS) macro the sources or the experiment patches (tools/exp/) test is in
+    the #error list the product build (-DRT_PRODUCT) checks, only rt_experiments.hpp names one among
+    the product sources, and the product rule defines RT_PRODUCT and no experiment macro."""
+    src = open(EXPERIMENTS).read()
     guard = src[src.index("#if defined(RT_PRODUCT) && (defined("):]
     guard = guard[:guard.index("#error")]
     listed = set(re.findall(r"defined\((RT_EXP_\w+|RT_KSTATS)\)", guard))
-    used = set(re.findall(r"#\s*(?:ifdef|ifndef|if\s+!?\s*defined\(|elif\s+defined\()\s*(RT_EXP_\w+|RT_KSTATS)", src))
-    used |= set(re.findall(r"defined\((RT_EXP_\w+)\)", src))
+    texts = [open(os.path.join(CSRC, f)).read() for f in _csrc_files()] + [open(p).read() for p in _patches()]
+    used = set()
+    for text in texts:
+        used |= set(re.findall(r"#\s*(?:ifdef|ifndef|if\s+!?\s*defined\(|elif\s+defined\()\s*(RT_EXP_\w+|RT_KSTATS)", text))
+        used |= set(re.findall(r"defined\((RT_EXP_\w+)\)", text))
     assert used and used <= listed, sorted(used - listed)
+    for f in _csrc_files():
+        if f != "rt_experiments.hpp":
+            assert "RT_EXP_" not in open(os.path.join(CSRC, f)).read(), f
     mk = open(MAKEFILE).read()
     rule = mk[mk.index("$(LIB): $(SRC) $(HDR)"):].split("\n\n")[0]
     assert "-DRT_PRODUCT" in rule and "RT_EXP" not in rule and "RT_EXPERIMENT" not in rule
     assert "RT_EXP" not in mk.split("HIPFLAGS ?=")[1].split("\n")[0]
+
+
+def test_experiment_patches_apply(tmp_path):
+    """The timing-experiment patches (tools/exp/*.patch, applied by `make exp`) apply cleanly to the
+    current sources, so an A/B build measures this tree."""
+    import shutil
+    for f in _csrc_files():
+        shutil.copy(os.path.join(CSRC, f), tmp_path / f)
+    assert _patches()
+    for p in _patches():
+        with open(p) as fh:
+            r = subprocess.run(["patch", "-s", "-p1", "-d", str(tmp_path)], stdin=fh, capture_output=True, text=True)
+        assert r.returncode == 0, (p, r.stdout, r.stderr)
 
 
 def test_experiment_library_is_refused(tmp_path):

@@ -26,8 +26,14 @@ def fuzz_bin(tmp_path_factory):
     return out
 
 
+def _kernel_src():
+    """Every csrc/ source of the library (one translation unit, split by stage)."""
+    d = os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc")
+    return "\n".join(open(os.path.join(d, f)).read() for f in sorted(os.listdir(d)) if f.endswith((".hip", ".hpp")))
+
+
 def test_margin_constant_matches_kernel():
-    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    src = _kernel_src()
     assert "kFilterMargin = 48.0f * 0x1.0p-24f" in src
     assert "KM = 48.0f * 0x1.0p-24f" in open(os.path.join(HERE, "filter_margin_fuzz.c")).read()
 
@@ -58,7 +64,7 @@ def cam_fuzz_bin(tmp_path_factory):
 
 
 def test_cam_margin_constant_matches_kernel():
-    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    src = _kernel_src()
     assert "sqrt(cd) - 0x1.8p-20 * ocn - 1e-20" in src      # 24 u |oc| + 1e-20
     assert "sqrt(c64) - 24 * u * ocn - 1e-20" in open(os.path.join(HERE, "cam_filter_fuzz.c")).read()
 
@@ -86,7 +92,7 @@ def cone_fuzz_bin(tmp_path_factory):
 
 
 def test_cone_margin_constant_matches_kernel():
-    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    src = _kernel_src()
     expr = "sqrt((double)r2 * (1.0 + 0x1.0p-20) + 0x1.0p-18 * wn2) + 0x1.0p-19 * sqrt(wn2) + 1e-30"   # 64 u, 32 u
     assert expr in src
     assert expr.replace("(double)r2 *", "r2t *") in open(os.path.join(HERE, "cone_cull_fuzz.c")).read()
@@ -123,7 +129,7 @@ def pixel_fuzz_bin(tmp_path_factory):
 
 
 def test_pixel_margin_matches_kernel():
-    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    src = _kernel_src()
     assert "const float margin = (M * 0x1.0p-20f) * __builtin_amdgcn_rsqf(dnc);" in src
     assert "1.0f + 0x1.0p-22f, 0x1.0p-21f + margin));" in src
     fz = open(os.path.join(HERE, "pixel_cone_fuzz.c")).read()
@@ -156,7 +162,7 @@ def box_fuzz_bin(tmp_path_factory):
 
 
 def test_box_margin_constants_match_kernel():
-    src = open(os.path.join(HERE, "..", "rust-ray-tracing_amd", "csrc", "rt_kernel.hip")).read()
+    src = _kernel_src()
     fz = open(os.path.join(HERE, "box_cull_fuzz.c")).read()
     assert "1.0f + __builtin_fmaf(m, qa.f_hir2, pm * qa.f_isr)" in src
     assert "p.f_hir2 = up32(0.5 / r2m)" in src and "p.f_isr = up32(8.0 * 0x1.0p-24 / std::sqrt(r2m))" in src

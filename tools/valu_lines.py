@@ -4,7 +4,7 @@
 Build the line-table assembly first:
   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -std=c++17 -gline-tables-only --cuda-device-only \
         -S -o rust-ray-tracing_amd/build/dbg.s rust-ray-tracing_amd/csrc/rt_kernel.hip
-Usage: valu_lines.py [kernel-substring] [first-line] [last-line] [asm]
+Usage: valu_lines.py [kernel-substring] [first-line] [last-line] [asm] [source file, default rt_sweep.hpp]
 """
 import collections
 import re
@@ -32,11 +32,12 @@ for line in body:
     k = "v" if op.startswith("v_") else "smem" if op.startswith("s_load") or op.startswith("s_buffer") else \
         "s" if op.startswith("s_") else "mem" if op.startswith(("global_", "ds_", "buffer_", "scratch_")) else "o"
     cnt[cur][k] += 1
-src = open("rust-ray-tracing_amd/csrc/rt_kernel.hip").read().split("\n")
+srcf = sys.argv[5] if len(sys.argv) > 5 else "rt_sweep.hpp"
+src = open("rust-ray-tracing_amd/csrc/" + srcf).read().split("\n")
 tot = collections.Counter()
 for c in cnt.values():
     tot.update(c)
 print(name, dict(tot))
 for (f, ln), c in sorted(((k, v) for k, v in cnt.items() if k), key=lambda x: (x[0][0], x[0][1])):
-    if f.endswith("rt_kernel.hip") and lo <= ln <= hi:
+    if f.endswith(srcf) and lo <= ln <= hi:
         print(f"{ln:5d} v{c['v']:4d} s{c['s']:3d} m{c['smem'] + c['mem']:3d}  {src[ln - 1].strip()[:90]}")
