@@ -193,6 +193,8 @@ def main():
     # One process per GPU.  RT_BENCH_BACKEND=gloo (rehearsal only: several ranks sharing one GPU,
     # shards staged through host memory) exercises the same partition/gather/assembly code.
     backend = os.environ.get("RT_BENCH_BACKEND", "nccl")
+    if args.probe_dist:
+        backend = "gloo"   # the rehearsal exchanges CPU tensors and must not initialise the GPU
     device = 0
     if not args.probe_dist:
         device = local_rank % max(1, torch.cuda.device_count())
@@ -254,12 +256,14 @@ def main():
     sptr = ctypes.c_void_p(stream.cuda_stream)
     red_dev = "cuda" if backend == "nccl" else "cpu"
     dynamic = args.schedule == "dynamic"
-    n_chunks = args.chunks or 4 * world
+    n_chunks = min(args.chunks or 4 * world, H)   # every chunk holds at least one row (rt_render_async
+    #                                               rejects an empty range)
     if dynamic:
         store = parallel.default_store() if dist_on else None
         frame = torch.zeros((H, W, 3), dtype=torch.uint8, device="cuda")
         cbufs = [torch.zeros((parallel.rows_max(H, n_chunks), W, 3), dtype=torch.uint8, device="cuda") for _ in range(2)]
-    sched = {"steps": 0, "chunks": 0, "pixels": 0}   # dynamic: this leg's claims on this rank
+    # dynamic: this leg's claims on this rank, and the events around each chunk's launch (kernel time)
+    sched = {"steps": 0, "chunks": 0, "pixels": 0, "kev": []}
 
     def step_dynamic(flags, ev=None):
         """One frame under the dynamic schedule: claim a chunk, launch it, keep at most two chunks queued
@@ -272,6 +276,7 @@ def main():
         if ev:
             ev[0].record(stream)
         pend, k = [], 0
+        kev = sched["kev"]
         while True:
             if q is not None:
                 j = q.claim()
@@ -281,8 +286,12 @@ def main():
                 break
             tr = parallel.chunk_range(W, H, n_chunks, j)
             buf = cbufs[k % 2]
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
             abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tr),
                                                ctypes.c_void_p(buf.data_ptr()), None, sptr))
+            e1.record(stream)
+            kev.append((e0, e1))
             parallel.place_chunk(frame, buf, H, n_chunks, j)
             done = torch.cuda.Event()
             done.record(stream)
@@ -348,6 +357,7 @@ def main():
         abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(abi.RtStats())), allow=(abi.RT_ERR_RANGE,))
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
         sched["chunks"] = sched["pixels"] = 0
+        sched["kev"] = []
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
@@ -361,6 +371,10 @@ def main():
         st = abi.RtStats()
         rc = abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(st)), allow=(abi.RT_ERR_RANGE,))
         phase = [sum(e[i].elapsed_time(e[i + 1]) for e in evs) / args.steps for i in range(3)]   # ms per step
+        if dynamic:
+            # phase 0 spans the host's claims and its waits for the chunk two back (wall time on the
+            # stream); the kernel time is the sum of the chunks' launches
+            phase[0] = sum(a.elapsed_time(b) for a, b in sched["kev"]) / args.steps
         pix = sched["pixels"] / args.steps if dynamic else tile.row_count * W   # pixels this rank renders per step
         px_s = pix / (phase[0] / 1e3) if phase[0] > 0 else 0.0   # this rank's px/s (renderer.rs:339)
         mine = [elapsed, phase[0], phase[1], phase[2], float(st.ray_segments), px_s, pix, sched["chunks"] / args.steps]

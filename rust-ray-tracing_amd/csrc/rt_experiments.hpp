@@ -18,6 +18,7 @@
                             defined(RT_EXP_DUP_SCATTER) || defined(RT_EXP_DUP_SWEEP) || defined(RT_EXP_DUP_CLBOX) ||   \
                             defined(RT_EXP_DUP_FILTER) || defined(RT_EXP_DUP_SUPBOX) || defined(RT_EXP_DUP_MEGABOX) || \
                             defined(RT_EXP_DUP_PLIST) || defined(RT_EXP_DUP_REPLAY) || defined(RT_EXP_DUP_REDUCE) ||   \
+                            defined(RT_EXP_TIMELINE) || \
                             defined(RT_KSTATS))
 #error "an experiment macro in the product build"
 #endif

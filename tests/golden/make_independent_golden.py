@@ -8,6 +8,11 @@ fp64 path against them (GPU).  Each case: scene, camera parameters, max_bounces,
 linear f64 + rgb8 + ray segments.
 
   python tests/golden/make_independent_golden.py     # rewrites tests/golden/independent_v2.npz
+  python tests/golden/make_independent_golden.py baseline   # rewrites tests/golden/independent_baseline.npz
+
+The baseline set (round 4) pins the BASELINE.json configs at their real sizes: strided pixels of
+configs B, C, D and E (full image, camera, sphere count, spp and depth), in f64 (the reference's
+arithmetic) and fp32 (the headline path), each pixel -> linear + rgb8 + its ray segments.
 """
 import json
 import os
@@ -66,6 +71,43 @@ def camera(W, H, over):
                             p["defocus_angle"])
 
 
+OUT_BASELINE = os.path.join(HERE, "independent_baseline.npz")
+# name: (config, n pixels, precision); pixels spread over the frame by a golden-ratio stride
+BASELINE_CASES = {f"{c}_{p}": (c, n, p) for c, n in (("B", 64), ("C", 64), ("D", 32), ("E", 32)) for p in ("f64", "f32")}
+
+
+def baseline_pixels(W, H, n):
+    step = int(W * H * 0.6180339887498949)
+    return [(k * step) % (W * H) for k in range(n)]
+
+
+def main_baseline():
+    data, meta = {}, {}
+    for name, (cfg, n, prec) in BASELINE_CASES.items():
+        W, H, nsph, spp, depth = rt.scenes.CONFIGS[cfg]
+        flat = rt.scenes.config_scene(cfg).flatten()
+        p, cam = camera(W, H, {})
+        px = baseline_pixels(W, H, n)
+        lin, rgb, segs = [], [], []
+        t0 = time.time()
+        for q in px:   # per pixel, so each pixel's segment count is pinned too
+            l, c, s = iv.render(flat, cam, spp, depth, SEED, pixels=[q], prec=prec)
+            lin += l
+            rgb += c
+            segs.append(s)
+        print(f"{name}: {W}x{H} {nsph} spheres spp {spp} depth {depth} {prec}: {n} pixels, {sum(segs)} segments, "
+              f"{time.time() - t0:.1f} s", flush=True)
+        data[f"{name}_lin"] = np.array(lin, dtype=np.float64)
+        data[f"{name}_rgb"] = np.array(rgb, dtype=np.uint8)
+        data[f"{name}_pix"] = np.array(px, dtype=np.int64)
+        data[f"{name}_segs"] = np.array(segs, dtype=np.int64)
+        meta[name] = {"config": cfg, "W": W, "H": H, "spheres": nsph, "depth": depth, "spp": spp, "precision": prec,
+                      "camera": p, "seed": SEED, "pixels": len(px)}
+    data["meta"] = np.array(json.dumps(meta))
+    np.savez_compressed(OUT_BASELINE, **data)
+    print("wrote", OUT_BASELINE)
+
+
 def main():
     data = {}
     meta = {}
@@ -85,4 +127,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["baseline"]:
+        main_baseline()
+    else:
+        main()

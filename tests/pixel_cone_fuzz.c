@@ -1,4 +1,4 @@
-// Fuzz of the per-pixel camera cone (rt_kernel.hip: pixel_list), test infrastructure for
+// Fuzz of the per-pixel camera cone (rt_camera.hpp: pixel_list), test infrastructure for
 // tests/test_filter_margin.py.  Claims checked, for random cameras (Camera::new, ray_tracing.rs:27-62),
 // image sizes and pixels:
 //  (1) containment: every primary ray of the pixel as the kernel computes it in T (Camera::get_ray,
@@ -160,11 +160,15 @@ int main(int argc, char** argv) {
             } else {
                 const float fjx = i == 1 || i == 3 ? 1.0f - 0x1.0p-24f : (float)jx;
                 const float fjy = i == 1 || i == 2 ? 1.0f - 0x1.0p-24f : (float)jy;
-                const float s1 = ((float)col + fjx) / (float)W, s2 = ((float)row + fjy) / (float)H;
+                // the kernel's div_dim (rt_common.hpp): RN_f(RN_d(x * RN_d(1/W))) for W < 2^20 (equal to
+                // RN_f(x / W), tests/test_div_dim.py; modelled literally here)
+                const float s1 = (float)((double)((float)col + fjx) * (1.0 / (double)W));
+                const float s2 = (float)((double)((float)row + fjy) * (1.0 / (double)H));
                 float pc[3], vf[3];
                 for (int k = 0; k < 3; ++k) pc[k] = tl[k] + (tu[k] * s1 + tv[k] * s2);
                 for (int k = 0; k < 3; ++k) vf[k] = pc[k] - (float)ctr[k];
-                const float l = sqrtf(vf[0] * vf[0] + vf[1] * vf[1] + vf[2] * vf[2]);
+                // unit() (rt_device.hpp, Vec3::length + division, geometry.rs:106-112): no FMA
+                const float l = sqrtf((vf[0] * vf[0] + vf[1] * vf[1]) + vf[2] * vf[2]);
                 for (int k = 0; k < 3; ++k) D[i][k] = vf[k] / l;
             }
             // (1) containment, in double: sin of the angle between the ray and the fp32 axis

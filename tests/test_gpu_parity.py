@@ -240,6 +240,37 @@ def test_independent_golden(renderer):
         np.testing.assert_array_equal(rgb, z[f"{name}_rgb"], err_msg=name)
 
 
+def _baseline_cases():
+    import json
+    import os
+    z = np.load(os.path.join(GOLDEN, "independent_baseline.npz"), allow_pickle=False)
+    return z, json.loads(str(z["meta"]))
+
+
+@pytest.mark.parametrize("name", sorted(_baseline_cases()[1]))
+def test_independent_baseline_golden(renderer, name):
+    """The HIP kernel against the INDEPENDENT restatement at every BASELINE config's real size (B, C, D,
+    E: image, camera, sphere count, spp, depth), in fp64 AND fp32 (the headline path): strided pixels,
+    each launched as a 1x1 tile of the full frame, bit for bit, ray segments per pixel included
+    (tests/golden/independent_baseline.npz, make_independent_golden.py baseline)."""
+    z, meta = _baseline_cases()
+    m = meta[name]
+    flat = rt.scenes.config_scene(m["config"]).flatten()
+    cam = rt.camera_new_py(m["W"], m["H"], **m["camera"])
+    flags = abi.RT_FLAG_F32 if m["precision"] == "f32" else 0
+    lin_all, rgb_all = [], []
+    for k, q in enumerate(z[f"{name}_pix"]):
+        q = int(q)
+        tile = abi.RtTileRange(q // m["W"], 1, 1, q % m["W"], 1)
+        rgb, lin, st, rc = gpu(renderer, flat, cam, m["depth"], m["spp"], m["seed"], flags, tile=tile)
+        assert rc == 0, (name, q)
+        assert st.ray_segments == int(z[f"{name}_segs"][k]), (name, q)
+        lin_all.append(lin.reshape(3))
+        rgb_all.append(rgb.reshape(3))
+    np.testing.assert_array_equal(np.array(lin_all), z[f"{name}_lin"], err_msg=name)
+    np.testing.assert_array_equal(np.array(rgb_all), z[f"{name}_rgb"], err_msg=name)
+
+
 # ---------------------------------------------------------------- BASELINE sizes
 @pytest.mark.parametrize("config,flags", [("B", abi.RT_FLAG_F32), ("C", abi.RT_FLAG_F32), ("C", 0)])
 def test_full_size_configs(renderer, config, flags):

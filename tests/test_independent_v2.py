@@ -117,3 +117,100 @@ def test_goldens_regenerate():
         lin, rgb, segs = iv.render(_flat(m["scene"]), cam, m["spp"], m["depth"], m["seed"])
         assert segs == m["segments"]
         assert np.array_equal(np.array(lin), z[f"{name}_lin"]), name
+
+
+# ---- round 4: the BASELINE configs at their real sizes, f64 and fp32 ---------------------------------
+GOLDEN_BASELINE = os.path.join(HERE, "golden", "independent_baseline.npz")
+
+
+def _baseline():
+    z = np.load(GOLDEN_BASELINE, allow_pickle=False)
+    return z, json.loads(str(z["meta"]))
+
+
+def test_exact_fma32():
+    """iv.fma32 is the correctly rounded fp32 a*b+c (against Fraction arithmetic rounded to 24 bits by
+    numpy's own conversion of the exact value's nearest doubles, checked two-sided)."""
+    rng = random.Random(11)
+    F = np.float32
+    for _ in range(20000):
+        a = F(rng.uniform(-4, 4) * 2.0 ** rng.randint(-20, 20))
+        b = F(rng.uniform(-4, 4) * 2.0 ** rng.randint(-20, 20))
+        c = F(-float(a) * float(b) * (1 + rng.uniform(-1e-5, 1e-5))) if rng.random() < 0.5 else \
+            F(rng.uniform(-4, 4) * 2.0 ** rng.randint(-30, 30))
+        r = iv.fma32(a, b, c)
+        exact = Fraction(float(a)) * Fraction(float(b)) + Fraction(float(c))
+        if exact == 0:
+            assert r == 0
+            continue
+        # r is the fp32 nearest to exact: both neighbours are at least as far
+        lo, hi = np.nextafter(r, F(-np.inf)), np.nextafter(r, F(np.inf))
+        d = abs(Fraction(float(r)) - exact)
+        assert d <= abs(Fraction(float(lo)) - exact) and d <= abs(Fraction(float(hi)) - exact), (a, b, c)
+        if d == abs(Fraction(float(lo)) - exact) or d == abs(Fraction(float(hi)) - exact):   # a tie: even
+            assert (int(np.float32(r).view(np.uint32)) & 1) == 0
+
+
+@pytest.mark.parametrize("prec", ["f64", "f32"])
+def test_estimate_is_invisible(prec):
+    """hit_scene's numpy estimate (skipping spheres with a hopelessly negative discriminant) changes no
+    bit: the literal restatement (every sphere through the mul_add sequence) gives the same pixels."""
+    flat = rt.scenes.config_scene("C").flatten()
+    p = dict(rt.MAIN_CAMERA)
+    cam = iv.camera_new(24, 14, p["focal_length"], p["view_angle"], p["center"], p["look_at"], p["up"], 0.0)
+    px = [0, 5, 77, 150, 200, 321, 335]
+    a = iv.render(flat, cam, 8, 50, SEED, pixels=px, prec=prec)
+    b = iv.render(flat, cam, 8, 50, SEED, pixels=px, prec=prec, literal=True)
+    assert a[2] == b[2] and np.array_equal(np.array(a[0], dtype=np.float64), np.array(b[0], dtype=np.float64))
+    assert a[1] == b[1]
+
+
+@pytest.mark.parametrize("tag,W,H,spp,depth", [("A", 8, 5, 6, 8), ("S100", 4, 3, 12, 50), ("Q", 6, 4, 9, 50)])
+def test_fp32_restatement_matches_oracle(tag, W, H, spp, depth):
+    """The fp32 reading (every value a numpy float32, exact fp32 mul_add) against the C oracle's f32
+    build, bit for bit: the headline path's second pin."""
+    flat = _flat(tag)
+    p = dict(rt.MAIN_CAMERA)
+    cam_abi = rt.camera_new_py(W, H, **p)
+    cam = iv.camera_new(W, H, p["focal_length"], p["view_angle"], p["center"], p["look_at"], p["up"], p["defocus_angle"])
+    lin, rgb, segs = iv.render(flat, cam, spp, depth, SEED, prec="f32")
+    rgb_o, lin_o, segs_o, rc = oracle_render(flat, cam_abi, depth, spp, SEED, precision="f32")
+    assert rc == 0 and segs == segs_o
+    assert np.array_equal(np.array(lin, dtype=np.float64), lin_o)
+    assert np.array_equal(np.array(rgb, dtype=np.uint8), rgb_o)
+
+
+def test_oracle_matches_baseline_goldens():
+    """The C oracle (f64 and f32 builds) against the independent restatement's vectors at every BASELINE
+    config's real image size, sphere count, spp and depth (tests/golden/independent_baseline.npz)."""
+    z, meta = _baseline()
+    assert {m["config"] for m in meta.values()} >= {"B", "C", "D", "E"}
+    assert {m["precision"] for m in meta.values()} == {"f64", "f32"}
+    for name, m in meta.items():
+        flat = rt.scenes.config_scene(m["config"]).flatten()
+        cam = rt.camera_new_py(m["W"], m["H"], **m["camera"])
+        px = z[f"{name}_pix"]
+        rgb_o, lin_o, segs_o, rc = oracle_render(flat, cam, m["depth"], m["spp"], m["seed"],
+                                                 pixels=px.astype(np.uint32), precision=m["precision"])
+        assert rc == 0, name
+        assert segs_o == int(z[f"{name}_segs"].sum()), name
+        assert np.array_equal(lin_o, z[f"{name}_lin"]), name
+        assert np.array_equal(rgb_o, z[f"{name}_rgb"]), name
+        assert 1.0 < segs_o / (len(px) * m["spp"]) < 4.0, name   # not all sky
+
+
+def test_baseline_goldens_regenerate():
+    """The restatement still produces the committed baseline vectors (two pixels per precision)."""
+    z, meta = _baseline()
+    for name in ("C_f32", "B_f64"):
+        m = meta[name]
+        c = m["camera"]
+        cam = iv.camera_new(m["W"], m["H"], c["focal_length"], c["view_angle"], c["center"], c["look_at"], c["up"],
+                            c["defocus_angle"])
+        flat = rt.scenes.config_scene(m["config"]).flatten()
+        for k in (1, 2):
+            q = int(z[f"{name}_pix"][k])
+            lin, rgb, segs = iv.render(flat, cam, m["spp"], m["depth"], m["seed"], pixels=[q], prec=m["precision"])
+            assert segs == int(z[f"{name}_segs"][k]), name
+            assert np.array_equal(np.array(lin, dtype=np.float64), z[f"{name}_lin"][k:k + 1]), name
+            assert np.array_equal(np.array(rgb, dtype=np.uint8), z[f"{name}_rgb"][k:k + 1]), name
