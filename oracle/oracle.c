@@ -127,3 +127,6 @@ int oracle_camera_new(or_camera* out, uint32_t w, uint32_t h, double focal_lengt
     out->dv[0] = dv.x; out->dv[1] = dv.y; out->dv[2] = dv.z;
     return 0;
 }
+
+/* ---------------- the reference-shaped packed CPU baseline (explicit AVX2, 128x128 tiles) ---------------- */
+#include "packed_avx2.h"

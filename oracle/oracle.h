@@ -97,6 +97,14 @@ void oracle_to_u8(const double rgb[3], uint8_t out[3], int* panics);
 void oracle_get_ray_f64(const or_camera* cam, uint32_t col, uint32_t row, uint32_t sample,
                         uint64_t seed, double origin[3], double dir[3]);
 
+/* The reference-shaped CPU baseline (packed_avx2.h): the same results as oracle_render_f64, computed
+ * the way the reference runs them (4-lane f64 AVX2 packets, 128x128 tiles through a shared queue).
+ * rgb_out / lin_out are full-frame (W*H*3); only the listed tiles (row-major tile grid; NULL = all)
+ * are written. */
+int packed_render_f64(const or_scene* sc, const or_camera* cam, uint32_t max_bounces, uint32_t spp, uint64_t seed,
+                      uint32_t tile, const uint32_t* tiles, uint32_t n_tiles, uint8_t* rgb_out, double* lin_out,
+                      uint64_t* segments, uint64_t* pixels_out, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,3 +66,27 @@ def oracle_render(flat, cam, max_bounces, spp, seed, flags=0, pixels=None, preci
     rc = fn(ctypes.addressof(flat.abi), ctypes.addressof(cam), max_bounces, spp, seed, flags, pix_ptr, n,
             rgb.ctypes.data, lin.ctypes.data, ctypes.byref(segs), threads)
     return rgb, lin, segs.value, rc
+
+
+def packed_render(flat, cam, max_bounces, spp, seed, tiles=None, tile=128, threads=None, lib_path=None):
+    """The reference-shaped CPU baseline (oracle/packed_avx2.h, f64): 4-lane AVX2 packets, tile x tile
+    blocks through a shared queue.  tiles: block indices (row-major block grid) or None = all.
+    Returns (rgb [W*H,3] u8, linear [W*H,3] f64 -- only the rendered blocks written, segments, pixels, rc)."""
+    lib = load_oracle(lib_path)
+    fn = lib.packed_render_f64
+    vp, u32, u64 = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64
+    fn.argtypes = [vp, vp, u32, u32, u64, u32, vp, u32, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.c_int]
+    fn.restype = ctypes.c_int
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    n = cam.image_width * cam.image_height
+    rgb = np.zeros((n, 3), dtype=np.uint8)
+    lin = np.zeros((n, 3), dtype=np.float64)
+    tptr, nt = None, 0
+    if tiles is not None:
+        tiles = np.ascontiguousarray(tiles, dtype=np.uint32)
+        tptr, nt = tiles.ctypes.data, len(tiles)
+    segs, pix = u64(0), u64(0)
+    rc = fn(ctypes.addressof(flat.abi), ctypes.addressof(cam), max_bounces, spp, seed, tile, tptr, nt,
+            rgb.ctypes.data, lin.ctypes.data, ctypes.byref(segs), ctypes.byref(pix), threads)
+    return rgb, lin, segs.value, pix.value, rc
