@@ -114,9 +114,13 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // The position map in LDS (live-path kernels without the mega level, P <= kLMapCap positions: config C's
 // 512 spp): the replay's scattered u16 writes, the map's initialisation and the reduction's reads stay
 // on the CU instead of going to HBM as partial lines.  Larger P uses the global map in PScratch.
+// ihist (kernels with the incremental histogram, trace_paths): the slot's counts of e == k for k < 32
+// (u16 pairs, 16 words) and its largest e, kept by terminate as the samples end; pass 1 below then only
+// runs when the pixel's K exceeds 32.
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
-                                                 T (*stage)[64], uint16_t* lmap) {
+                                                 T (*stage)[64], uint16_t* lmap, const uint32_t* ihist = nullptr,
+                                                 uint32_t imaxe = 0u) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -143,12 +147,22 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // histogram of the termination bounces below 64 (a sample terminated iff e < depth, and then
     // e < K); it is only used when K <= 64.
     uint32_t K = 0;
-    const bool hist_on = MODE == kModeV2 && depth > 0u;
+    bool counted = false;   // K and the histogram from the incremental counts
+    if (MODE == kModeV2 && ihist != nullptr && depth > 0u) {
+        const uint32_t Ki = min(depth, imaxe + 1u);
+        if (Ki <= 32u) {
+            K = Ki;
+            counted = true;
+            const uint32_t w = lane < 32u ? ihist[lane >> 1] : 0u;
+            hist[lane] = (w >> ((lane & 1u) << 4)) & 0xFFFFu;
+        }
+    }
+    const bool hist_on = MODE == kModeV2 && depth > 0u && !counted;
     if (hist_on) {
         hist[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
     }
-    if (depth > 0) {
+    if (depth > 0 && !counted) {
         uint32_t me = 0;
         for (uint32_t b = 0; b < spp; b += 512u) {
             uint32_t ev[8];

@@ -96,10 +96,22 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // into the hot loop at 80 VGPRs); the mega kernels' LDS is full at 6 waves per SIMD.
     constexpr bool kLMap = MODE == kModeV2 && !MEGA && kLMapCap > 0u && sizeof(T) == 8 && !kF64Park;
     __shared__ __attribute__((aligned(16))) uint16_t s_lmap[kLMap ? 4 : 1][kLMap ? kLMapCap : 2];
+    // The live path's per-slot histogram of the termination bounces below 32 (u16 pairs) and the
+    // slot's largest bounce, counted as samples end (terminate), so finish_pixel skips its first pass
+    // over the records for pixels with K <= 32 (C: 4.5 bounce iterations per pixel on average).  Not in
+    // the mega kernels (their LDS is full at 6 waves per SIMD) nor at W7; spp <= 65535 keeps a u16
+    // count from carrying into its neighbour.
+    constexpr bool kIncHist = MODE == kModeV2 && !MEGA && W <= 6;
+    __shared__ uint32_t s_ih[kIncHist ? 4 : 1][kIncHist ? kSlots : 1][kIncHist ? 17 : 1];   // [16]: largest e
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
     if (lane < kNWork) g_work[wave][lane] = 0ull;
+    if constexpr (kIncHist) {
+        for (uint32_t i = lane; i < kSlots * 17u; i += 64u) (&s_ih[wave][0][0])[i] = 0u;
+    }
+    // read at each use (a kernel argument through the laundered pointer: no SGPR held across the loop)
+    auto inc_hist = [&]() -> bool { return kIncHist && cold_args<T>()->spp <= 65535u; };
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
@@ -223,6 +235,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
             sc.set_e(t_slot, t_sid, e);
+            if (inc_hist()) {   // the slot's incremental histogram (e < depth: a sky hit) and largest e
+                if (skyhit && e < 32u) atomicAdd(&s_ih[wave][t_slot][e >> 1], 1u << ((e & 1u) << 4));
+                atomicMax(&s_ih[wave][t_slot][16], e);
+            }
             if (MODE == kModeV2) {
                 // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
                 // the copies into them raised the register peak (spills in the sphere sweeps).  A sky
@@ -246,8 +262,14 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (__builtin_expect(__builtin_amdgcn_readlane(slot_left, s) == 0u, 0)) {
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
-                const uint32_t K = finish_pixel<T, MODE>(wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s),
-                                                         s_hist[wave], s_stage[wave], kLMap ? s_lmap[wave] : nullptr);
+                const bool ih = inc_hist();
+                const uint32_t K = finish_pixel<T, MODE>(
+                    wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave], s_stage[wave],
+                    kLMap ? s_lmap[wave] : nullptr, ih ? s_ih[wave][s] : nullptr,
+                    ih ? __builtin_amdgcn_readfirstlane(s_ih[wave][s][16]) : 0u);
+                if (ih) {   // the slot is free again: its counts restart at zero
+                    if (lane < 17u) s_ih[wave][s][lane] = 0u;
+                }
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
