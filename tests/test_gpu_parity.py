@@ -202,7 +202,7 @@ def _golden_cases():
     return mg
 
 
-@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f != "independent_v2.npz"))
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("independent")))
 def test_golden_fixtures_gpu(renderer, name):
     mg = _golden_cases()
     tag, w, h, depth, spp, flags, prec, _ = mg.CASES[name]

@@ -209,7 +209,7 @@ def test_fp32_tracks_fp64_statistically():
     assert rmse < noise
 
 
-@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and f != "independent_v2.npz"))
+@pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("independent")))
 def test_golden_fixtures(name):
     """The oracle reproduces every committed golden fixture bit-for-bit (drift guard)."""
     import importlib.util
