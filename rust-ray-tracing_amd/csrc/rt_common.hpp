@@ -172,6 +172,11 @@ __device__ __forceinline__ void work_add(uint32_t i, uint32_t n) {
 }
 
 
+// #{set bits of m in the lanes below this one}: v_mbcnt_lo/hi, no lane mask held in VGPRs
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // Uniform (scalar-cache) view of a read-only kernel buffer: the sphere loop index is
 // wave-uniform, so these become s_load into SGPRs — a free broadcast to all 64 lanes.
 template <typename T> using cptr = const __attribute__((address_space(4))) T*;

@@ -123,7 +123,6 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                                                  uint32_t imaxe = 0u) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
     constexpr uint32_t kNone = PScratch<T>::kNone;
     const bool lm = kLMapCap > 0u && lmap != nullptr && P <= kLMapCap;   // wave-uniform
@@ -240,8 +239,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 if (ret) {
                     // Sample i, terminated at bounce e, sat at pold = #{s' < i : e_s' >= e} during bounce e
                     // and moves to pnew = n_{e+1} + #{s' < i : e_s' == e}
-                    const uint32_t pold = cg + (uint32_t)__popcll((gt | eq) & lt_mask);
-                    const uint32_t pnew = nn + cq + (uint32_t)__popcll(eq & lt_mask);
+                    const uint32_t pold = cg + lanes_below(gt | eq);
+                    const uint32_t pnew = nn + cq + lanes_below(eq);
                     const uint32_t Lnext = ek + 1u == depth ? 0u : (nn + 3u) / 4u;
                     // positions [lo, 4 ceil(n_k / 4)) retire at bounce e; pold and pnew are below n_k <= 4 Lk (pold
                     // counts the earlier samples with e >= k, pnew = n_{k+1} + the earlier ones with
@@ -292,7 +291,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const uint32_t smp = in ? sig[qq] : 0u;
                 const bool en = in && enabled(qq, smp), dis = in && !en;
                 const unsigned long long bd = __ballot(dis), be = __ballot(en);
-                const uint32_t rd = cd + (uint32_t)__popcll(bd & lt_mask), rf = ce + (uint32_t)__popcll(be & lt_mask);
+                const uint32_t rd = cd + lanes_below(bd), rf = ce + lanes_below(be);
                 if (in && (qq & 3u) == 0u) Jl = max(Jl, min(rd, ne - rf));   // boundary c = qq / 4
                 if (dis && rd < P / 2u) tabD[rd] = smp;
                 if (en && ne - 1u - rf < P / 2u) tabE[ne - 1u - rf] = smp;
@@ -309,7 +308,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const uint32_t smp = in ? sig[qq] : 0u;
                 const bool en = in && enabled(qq, smp), dis = in && !en;
                 const unsigned long long bd = __ballot(dis), be = __ballot(en);
-                const uint32_t rd = cd + (uint32_t)__popcll(bd & lt_mask), re = ne - 1u - (ce + (uint32_t)__popcll(be & lt_mask));
+                const uint32_t rd = cd + lanes_below(bd), re = ne - 1u - (ce + lanes_below(be));
                 if (dis && rd < J) sig[qq] = tabE[rd];
                 if (en && re < J) sig[qq] = tabD[re];
                 if ((en && re == J) || (dis && rd + 1u == J)) back = max(back, qq + 1u);
@@ -346,8 +345,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const bool ge = i < spp && e >= k, eq = e == k;
                 const unsigned long long bge = __ballot(ge), beq = __ballot(eq);
                 if (eq) {
-                    const uint32_t pold = cge + (uint32_t)__popcll(bge & lt_mask);
-                    const uint32_t pnew = n_next + ceq + (uint32_t)__popcll(beq & lt_mask);
+                    const uint32_t pold = cge + lanes_below(bge);
+                    const uint32_t pnew = n_next + ceq + lanes_below(beq);
                     const bool w_old = U && pold >= lo;   // pold, pnew < n_k <= hi (as above)
                     const bool w_new = !U || pnew < lo;
                     // At most one position except when the old one retires now and the new one later.

@@ -80,6 +80,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
     __shared__ uint32_t q_sid[QW][QN];   // sid | slot << 29 (the pixel: s_slotpix[slot])
     __shared__ uint32_t s_slotpix[4][kSlots];   // the pixel of each open slot
+    // ... its work item and its samples not yet terminated (read where needed, not held in VGPRs)
+    __shared__ uint32_t s_item[4][kSlots], s_left[4][kSlots];
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
     // camera candidate list of each open pixel slot (pixel_list): [0] = count (0xFFFF: none, sweep per batch)
@@ -115,17 +117,19 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
-    const unsigned long long lt_mask = (1ull << lane) - 1ull;
     if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
     if (threadIdx.x == 0) s_pool = 0ull;   // {next, end} = {0, 0}: empty
     __syncthreads();
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
-    uint32_t sid = 0, k = 0, slot = 0, pix = 0;
+    // the lane's sample and pixel slot in one VGPR, sid | slot << 29 (as in the camera queue: spp <= 2^20,
+    // kSlots <= 8); the slot's pixel is read from s_slotpix where the scatter needs it
+    uint32_t ss = 0, k = 0;
+    auto sid_of = [](uint32_t v) -> uint32_t { return v & 0x1FFFFFFFu; };
+    auto slot_of = [](uint32_t v) -> uint32_t { return v >> 29; };
     bool live = false;
     bool scat = false;                 // hit at bounce k last iteration, still below depth: scatter now
     int hit_i = -1;
     T hit_t = T(0);
-    uint32_t slot_item = 0, slot_left = 0;   // lane s < kSlots: pixel item and unfinished samples of slot s
     auto park = [&](const V3<T>& po, const V3<T>& pd) {
         T* r = &s_park[kPark ? wave : 0][0][lane];
         r[0] = po.x; r[64] = po.y; r[128] = po.z; r[192] = pd.x; r[256] = pd.y; r[320] = pd.z;
@@ -204,8 +208,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 cur_row = q.row_begin + ri * q.row_step;
                 cur_col = q.col_begin + ci;
                 cur_pix = cur_row * q.W + cur_col;
-                if (lane == s) { slot_item = item; slot_left = spp; }
-                if (lane == 0) s_slotpix[wave][s] = cur_pix;
+                if (lane == 0) { s_slotpix[wave][s] = cur_pix; s_item[wave][s] = item; s_left[wave][s] = spp; }
                 busy |= 1u << s;
                 opened |= 1u << s;
                 cur = s;
@@ -213,7 +216,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             }
             const bool isw = (want >> lane) & 1ull;
             const uint32_t take = min((uint32_t)__popcll(want), spp - cur_next);
-            const uint32_t r = (uint32_t)__popcll(want & lt_mask);
+            const uint32_t r = lanes_below(want);
             const bool mine = isw && r < take;
             if (mine) { got = true; i_sid = cur_next + r; i_slot = cur; i_pix = cur_pix; i_row = cur_row; i_col = cur_col; }
             want &= ~__ballot(mine);
@@ -256,15 +259,16 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t s = __builtin_amdgcn_readlane(t_slot, __builtin_ctzll(tm));
             const unsigned long long m = __ballot(term && t_slot == s);
             tm &= ~m;
-            if (lane == s) slot_left -= (uint32_t)__popcll(m);
+            const uint32_t left = __builtin_amdgcn_readfirstlane(s_left[wave][s]) - (uint32_t)__popcll(m);
+            if (lane == 0) s_left[wave][s] = left;
             // pixel complete: once per spp samples -- marked unlikely, so the register allocator
             // places any spill code here rather than in the sphere sweeps
-            if (__builtin_expect(__builtin_amdgcn_readlane(slot_left, s) == 0u, 0)) {
+            if (__builtin_expect(left == 0u, 0)) {
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
                 const bool ih = inc_hist();
                 const uint32_t K = finish_pixel<T, MODE>(
-                    wave_scratch<T>(wave), s, __builtin_amdgcn_readlane(slot_item, s), s_hist[wave], s_stage[wave],
+                    wave_scratch<T>(wave), s, __builtin_amdgcn_readfirstlane(s_item[wave][s]), s_hist[wave], s_stage[wave],
                     kLMap ? s_lmap[wave] : nullptr, ih ? s_ih[wave][s] : nullptr,
                     ih ? __builtin_amdgcn_readfirstlane(s_ih[wave][s][16]) : 0u);
                 if (ih) {   // the slot is free again: its counts restart at zero
@@ -335,7 +339,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
         const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
         if (push) {
-            const uint32_t e = (qhead + qcount + (uint32_t)__popcll(pm & lt_mask)) % QN;
+            const uint32_t e = (qhead + qcount + lanes_below(pm)) % QN;
             q_sid[wave][e] = bsid | (bslot << 29);
             q_hit[wave][e] = bi;
             q_t[wave][e] = bt;
@@ -348,7 +352,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
 
     for (;;) {
         bool fresh = false;
-        uint32_t frow = 0, fcol = 0;
+        uint32_t frow = 0, fcol = 0, npix = 0;
         if constexpr (CAMQ) {
             // ---- top up the queue with camera batches, then free lanes pop primary-ray hits ----
             const unsigned long long freem = __ballot(!live);
@@ -361,13 +365,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t qhead = __builtin_amdgcn_readfirstlane(s_is[wave].qhead);
             const uint32_t qcount = __builtin_amdgcn_readfirstlane(s_is[wave].qcount);
             const uint32_t take = min(nfree, qcount);
-            const uint32_t r = (uint32_t)__popcll(freem & lt_mask);
+            const uint32_t r = lanes_below(freem);
             if (!live && r < take) {
                 const uint32_t e = (qhead + r) % QN;
-                const uint32_t w0 = q_sid[wave][e];
-                sid = w0 & 0x1FFFFFFFu;
-                slot = w0 >> 29;
-                pix = s_slotpix[wave][slot];
+                ss = q_sid[wave][e];
                 hit_i = q_hit[wave][e];
                 hit_t = q_t[wave][e];
                 const auto& q = *cold_args<T>();
@@ -384,20 +385,23 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (lane == 0) { s_is[wave].qhead = (qhead + take) % QN; s_is[wave].qcount = qcount - take; }
         } else {
             // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
-            uint32_t nsid = 0, nslot = 0, npix = 0;
+            uint32_t nsid = 0, nslot = 0;
             fresh = issue(__ballot(!live), nsid, nslot, npix, frow, fcol);
-            if (fresh) { sid = nsid; slot = nslot; pix = npix; }
+            if (fresh) ss = nsid | (nslot << 29);
         }
         // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
         if constexpr (kPark) unpark(o, d);
         if constexpr (kParkC) c = unpark_c();
-        if (fresh || scat) next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid, k, hit_i, hit_t, o, d, c);
+        if (fresh || scat) {
+            const uint32_t pix = (!CAMQ && fresh) ? npix : s_slotpix[wave][slot_of(ss)];
+            next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid_of(ss), k, hit_i, hit_t, o, d, c);
+        }
         if constexpr (kPark) park(o, d);
         if constexpr (kParkC) park_c(c);
         if (fresh) {
             k = 0;
             live = true;
-            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot, sid) = d.y;   // primary y, kept for quirk Q2
+            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot_of(ss), sid_of(ss)) = d.y;   // primary y (quirk Q2)
         } else if (scat) {
             k += 1u;
         }
@@ -419,7 +423,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (MODE != kModeV2) { V3<T> po, pd; unpark(po, pd); d = pd; }   // the own-value modes read d
         }
         if constexpr (kParkC) c = unpark_c();
-        terminate(term, skyhit, skyhit ? k : depth, slot, sid, c, d);
+        terminate(term, skyhit, skyhit ? k : depth, slot_of(ss), sid_of(ss), c, d);
         live = live && !term;
     }
     if (lane == 0) {
