@@ -100,10 +100,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lmap[kLMap ? 4 : 1][kLMap ? kLMapCap : 2];
     // The live path's per-slot histogram of the termination bounces below 32 (u16 pairs) and the
     // slot's largest bounce, counted as samples end (terminate), so finish_pixel skips its first pass
-    // over the records for pixels with K <= 32 (C: 4.5 bounce iterations per pixel on average).  Not in
-    // the mega kernels (their LDS is full at 6 waves per SIMD) nor at W7; spp <= 65535 keeps a u16
-    // count from carrying into its neighbour.
-    constexpr bool kIncHist = MODE == kModeV2 && !MEGA && W <= 6;
+    // over the records for pixels with K <= 32 (C: 4.5 bounce iterations per pixel on average).  Not
+    // where the LDS is full: the mega kernels at 6 waves per SIMD, fp64 at 5+ (32 KB per workgroup), W7;
+    // spp <= 65535 keeps a u16 count from carrying into its neighbour.
+    constexpr bool kIncHist = MODE == kModeV2 && !MEGA && W <= 6 && !kF64Park;
     __shared__ uint32_t s_ih[kIncHist ? 4 : 1][kIncHist ? kSlots : 1][kIncHist ? 17 : 1];   // [16]: largest e
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
