@@ -101,6 +101,11 @@ struct rt_context {
     uint64_t samples = 0, pixels = 0;
     hipStream_t last_stream = nullptr;   // stream of the previous render (they share scratch and tables)
     bool have_last = false;
+    // The camera tables of each precision (build_cam_table) depend only on the scene, the camera centre,
+    // the scalar mode and RT_FILTER_OFF: a launch with the same key reuses them (bench frames, shards).
+    uint64_t scene_gen = 0;
+    struct CamKey { bool valid = false; uint64_t gen = 0; double center[3] = {0, 0, 0}; uint32_t scalar = 0, off = 0; };
+    CamKey camkey[2];   // [0] fp32 tables, [1] fp64
 };
 
 extern "C" const char* rt_last_error(void) { return g_err.c_str(); }
@@ -226,6 +231,8 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipStreamSynchronize(c->stream));
     free_scene(c);
+    ++c->scene_gen;   // camera tables built for the previous scene are stale
+    c->camkey[0].valid = c->camkey[1].valid = false;
     std::vector<double> g64, c64; std::vector<MatT<double>> m64;
     std::vector<float> g32, c32; std::vector<MatT<float>> m32;
     pack_scene(s, g64, c64, m64, c->n_groups64);
@@ -536,12 +543,24 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         p.n_supc = c->n_supc;
         const uint32_t n_thr = std::max(std::max(std::max(n_slots, n_fslots), c->n_cull),
                                         std::max(c->n_cslots, c->n_clp + c->n_supc));
-        auto build = (flags & RT_FLAG_MODE_SCALAR) ? build_cam_table<T, true> : build_cam_table<T, false>;
-        hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
-                           (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off,
-                           (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres, c->ridx, c->n_cslots,
-                           (const double*)(f64 ? c->clus64 : c->clus32), (float*)p.cullc, c->n_clp + c->n_supc);
-        HIPCHK(hipGetLastError());
+        rt_context::CamKey& ck = c->camkey[f64 ? 1 : 0];
+        const uint32_t scalar = (flags & RT_FLAG_MODE_SCALAR) ? 1u : 0u;
+        double cen[3] = {(double)p.center[0], (double)p.center[1], (double)p.center[2]};
+        const bool same = ck.valid && ck.gen == c->scene_gen && ck.scalar == scalar && ck.off == (uint32_t)filter_off &&
+                          memcmp(ck.center, cen, sizeof(cen)) == 0;   // bit for bit (-0 is not +0)
+        if (!same) {
+            auto build = scalar ? build_cam_table<T, true> : build_cam_table<T, false>;
+            hipLaunchKernelGGL(build, dim3((n_thr + 255) / 256), dim3(256), 0, st, p.sph, (T*)p.camsph, n_slots,
+                               (float*)p.camf, n_fslots, p.center[0], p.center[1], p.center[2], (uint32_t)filter_off,
+                               (T*)p.camx, (float*)p.cull, c->n_cull, c->n_spheres, c->ridx, c->n_cslots,
+                               (const double*)(f64 ? c->clus64 : c->clus32), (float*)p.cullc, c->n_clp + c->n_supc);
+            HIPCHK(hipGetLastError());
+            ck.valid = true;
+            ck.gen = c->scene_gen;
+            ck.scalar = scalar;
+            ck.off = (uint32_t)filter_off;
+            memcpy(ck.center, cen, sizeof(cen));
+        }
     }
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));

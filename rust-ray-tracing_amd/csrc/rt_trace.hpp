@@ -118,7 +118,14 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
     if (lane == 0) s_is[wave] = IssueState{0u, 0u, cold_args<T>()->spp, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    if (threadIdx.x == 0) s_pool = 0ull;   // {next, end} = {0, 0}: empty
+    // The workgroup's first block is block blockIdx.x, taken without an atomic (the counter's claims
+    // start at gridDim.x): the launch's opening burst of one global atomic per workgroup is gone.
+    {
+        const auto& q = *cold_args<T>();
+        uint32_t b0 = 0, b1 = 0;
+        const bool got = guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, blockIdx.x, b0, b1);
+        if (threadIdx.x == 0) s_pool = got ? ((unsigned long long)b0 << 32) | b1 : 0ull;   // {next, end}; {0, 0}: empty
+    }
     __syncthreads();
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
     // the lane's sample and pixel slot in one VGPR, sid | slot << 29 (as in the camera queue: spp <= 2^20,
@@ -185,7 +192,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                             pv = old;
                         }
                         if (it == 0xFFFFFFFFu) {
-                            const uint32_t j = atomicAdd(q.counter, 1u);
+                            const uint32_t j = atomicAdd(q.counter, 1u) + gridDim.x;
                             uint32_t b0 = 0, b1 = 0;
                             if (guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, j, b0, b1)) {
                                 it = b0;
