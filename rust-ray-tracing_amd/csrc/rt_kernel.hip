@@ -576,6 +576,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
                                                std::min<uint64_t>((uint64_t)kMaxBlock, (kClaimSpp + spp - 1) / spp)});
         uint32_t G = 1;
         while (2u * G <= g) G *= 2u;
+        // diagnostics (tools/waves_ab.py --block): RT_BLOCK_G overrides the largest block (1..16, a power of two)
+        const char* ge = getenv("RT_BLOCK_G");
+        if (ge && atoi(ge) >= 1 && atoi(ge) <= (int)kMaxBlock && (atoi(ge) & (atoi(ge) - 1)) == 0) G = (uint32_t)atoi(ge);
         p.blk_g = G;
     }
     p.swide = paths_wide(p.P, depth);
