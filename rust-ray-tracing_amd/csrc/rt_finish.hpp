@@ -114,13 +114,9 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 // The position map in LDS (live-path kernels without the mega level, P <= kLMapCap positions: config C's
 // 512 spp): the replay's scattered u16 writes, the map's initialisation and the reduction's reads stay
 // on the CU instead of going to HBM as partial lines.  Larger P uses the global map in PScratch.
-// ihist (kernels with the incremental histogram, trace_paths): the slot's counts of e == k for k < 32
-// (u16 pairs, 16 words) and its largest e, kept by terminate as the samples end; pass 1 below then only
-// runs when the pixel's K exceeds 32.
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
-                                                 T (*stage)[64], uint16_t* lmap, const uint32_t* ihist = nullptr,
-                                                 uint32_t imaxe = 0u) {
+                                                 T (*stage)[64], uint16_t* lmap) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
@@ -145,23 +141,15 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // Bounce iterations the reference runs: K = min(depth, max e + 1).  The same pass builds the
     // histogram of the termination bounces below 64 (a sample terminated iff e < depth, and then
     // e < K); it is only used when K <= 64.
+    // (An incremental histogram kept by terminate as samples end, skipping this pass, measured -1.7 %
+    // at config C fp32 and -1.0 % fp64: its per-termination LDS atomics cost more than the pass.)
     uint32_t K = 0;
-    bool counted = false;   // K and the histogram from the incremental counts
-    if (MODE == kModeV2 && ihist != nullptr && depth > 0u) {
-        const uint32_t Ki = min(depth, imaxe + 1u);
-        if (Ki <= 32u) {
-            K = Ki;
-            counted = true;
-            const uint32_t w = lane < 32u ? ihist[lane >> 1] : 0u;
-            hist[lane] = (w >> ((lane & 1u) << 4)) & 0xFFFFu;
-        }
-    }
-    const bool hist_on = MODE == kModeV2 && depth > 0u && !counted;
+    const bool hist_on = MODE == kModeV2 && depth > 0u;
     if (hist_on) {
         hist[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
     }
-    if (depth > 0 && !counted) {
+    if (depth > 0) {
         uint32_t me = 0;
         for (uint32_t b = 0; b < spp; b += 512u) {
             uint32_t ev[8];

@@ -80,8 +80,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
     __shared__ uint32_t q_sid[QW][QN];   // sid | slot << 29 (the pixel: s_slotpix[slot])
     __shared__ uint32_t s_slotpix[4][kSlots];   // the pixel of each open slot
-    // ... its work item and its samples not yet terminated (read where needed, not held in VGPRs)
-    __shared__ uint32_t s_item[4][kSlots], s_left[4][kSlots];
+    // ... and its work item (read at finish_pixel, not held in a VGPR)
+    __shared__ uint32_t s_item[4][kSlots];
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
     // camera candidate list of each open pixel slot (pixel_list): [0] = count (0xFFFF: none, sweep per batch)
@@ -98,22 +98,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // into the hot loop at 80 VGPRs); the mega kernels' LDS is full at 6 waves per SIMD.
     constexpr bool kLMap = MODE == kModeV2 && !MEGA && kLMapCap > 0u && sizeof(T) == 8 && !kF64Park;
     __shared__ __attribute__((aligned(16))) uint16_t s_lmap[kLMap ? 4 : 1][kLMap ? kLMapCap : 2];
-    // The live path's per-slot histogram of the termination bounces below 32 (u16 pairs) and the
-    // slot's largest bounce, counted as samples end (terminate), so finish_pixel skips its first pass
-    // over the records for pixels with K <= 32 (C: 4.5 bounce iterations per pixel on average).  Not
-    // where the LDS is full: the mega kernels at 6 waves per SIMD, fp64 at 5+ (32 KB per workgroup), W7;
-    // spp <= 65535 keeps a u16 count from carrying into its neighbour.
-    constexpr bool kIncHist = MODE == kModeV2 && !MEGA && W <= 6 && !kF64Park;
-    __shared__ uint32_t s_ih[kIncHist ? 4 : 1][kIncHist ? kSlots : 1][kIncHist ? 17 : 1];   // [16]: largest e
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
     if (lane < kNWork) g_work[wave][lane] = 0ull;
-    if constexpr (kIncHist) {
-        for (uint32_t i = lane; i < kSlots * 17u; i += 64u) (&s_ih[wave][0][0])[i] = 0u;
-    }
-    // read at each use (a kernel argument through the laundered pointer: no SGPR held across the loop)
-    auto inc_hist = [&]() -> bool { return kIncHist && cold_args<T>()->spp <= 65535u; };
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
 #endif
@@ -131,6 +119,9 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // the lane's sample and pixel slot in one VGPR, sid | slot << 29 (as in the camera queue: spp <= 2^20,
     // kSlots <= 8); the slot's pixel is read from s_slotpix where the scatter needs it
     uint32_t ss = 0, k = 0;
+    // lane s < kSlots: slot s's samples not yet terminated.  In a VGPR, not LDS: the LDS round trip sat
+    // on terminate's path every iteration (config E -4.6 %, C +-0 against this)
+    uint32_t slot_left = 0;
     auto sid_of = [](uint32_t v) -> uint32_t { return v & 0x1FFFFFFFu; };
     auto slot_of = [](uint32_t v) -> uint32_t { return v >> 29; };
     bool live = false;
@@ -215,7 +206,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 cur_row = q.row_begin + ri * q.row_step;
                 cur_col = q.col_begin + ci;
                 cur_pix = cur_row * q.W + cur_col;
-                if (lane == 0) { s_slotpix[wave][s] = cur_pix; s_item[wave][s] = item; s_left[wave][s] = spp; }
+                if (lane == 0) { s_slotpix[wave][s] = cur_pix; s_item[wave][s] = item; }
+                if (lane == s) slot_left = spp;
                 busy |= 1u << s;
                 opened |= 1u << s;
                 cur = s;
@@ -245,10 +237,6 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (term) {
             const PScratch<T> sc = wave_scratch<T>(wave);
             sc.set_e(t_slot, t_sid, e);
-            if (inc_hist()) {   // the slot's incremental histogram (e < depth: a sky hit) and largest e
-                if (skyhit && e < 32u) atomicAdd(&s_ih[wave][t_slot][e >> 1], 1u << ((e & 1u) << 4));
-                atomicMax(&s_ih[wave][t_slot][16], e);
-            }
             if (MODE == kModeV2) {
                 // three dword stores, not one dwordx3: a dwordx3 wants three consecutive VGPRs, and
                 // the copies into them raised the register peak (spills in the sphere sweeps).  A sky
@@ -266,21 +254,16 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t s = __builtin_amdgcn_readlane(t_slot, __builtin_ctzll(tm));
             const unsigned long long m = __ballot(term && t_slot == s);
             tm &= ~m;
-            const uint32_t left = __builtin_amdgcn_readfirstlane(s_left[wave][s]) - (uint32_t)__popcll(m);
-            if (lane == 0) s_left[wave][s] = left;
+            if (lane == s) slot_left -= (uint32_t)__popcll(m);
+            const uint32_t left = __builtin_amdgcn_readlane(slot_left, s);
             // pixel complete: once per spp samples -- marked unlikely, so the register allocator
             // places any spill code here rather than in the sphere sweeps
             if (__builtin_expect(left == 0u, 0)) {
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
-                const bool ih = inc_hist();
                 const uint32_t K = finish_pixel<T, MODE>(
                     wave_scratch<T>(wave), s, __builtin_amdgcn_readfirstlane(s_item[wave][s]), s_hist[wave], s_stage[wave],
-                    kLMap ? s_lmap[wave] : nullptr, ih ? s_ih[wave][s] : nullptr,
-                    ih ? __builtin_amdgcn_readfirstlane(s_ih[wave][s][16]) : 0u);
-                if (ih) {   // the slot is free again: its counts restart at zero
-                    if (lane < 17u) s_ih[wave][s][lane] = 0u;
-                }
+                    kLMap ? s_lmap[wave] : nullptr);
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
