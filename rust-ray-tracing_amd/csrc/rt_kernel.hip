@@ -94,7 +94,7 @@ struct rt_context {
     uint32_t n_spheres = 0, n_materials = 0;
     unsigned long long* segs = nullptr;
     uint32_t* err = nullptr;
-    uint32_t* counter = nullptr;   // persistent-kernel block counter (zeroed before each launch)
+    uint32_t* counter = nullptr;   // persistent-kernel claim-stream counters (zeroed before each launch)
     void* scratch = nullptr;       // per-wave ray state (grown on demand)
     size_t scratch_bytes = 0;
     int n_cu = 0;
@@ -159,7 +159,7 @@ extern "C" int rt_context_create(int device, rt_context** out) {
     HIPCHK(hipEventCreate(&c->ev_last));
     HIPCHK(hipMalloc((void**)&c->segs, sizeof(unsigned long long) * kSegShards * kSegStride));
     HIPCHK(hipMalloc((void**)&c->err, 16));
-    HIPCHK(hipMalloc((void**)&c->counter, 16));
+    HIPCHK(hipMalloc((void**)&c->counter, kStreams * kCtrStride * sizeof(uint32_t)));   // claim streams (rt_trace.hpp)
     HIPCHK(hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, device));
     HIPCHK(hipMemset(c->segs, 0, sizeof(unsigned long long) * kSegShards * kSegStride));
     HIPCHK(hipMemset(c->err, 0, 16));
@@ -592,7 +592,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     const int rc = ensure_scratch(c, p.scratch_stride * nblocks * 4, st);
     if (rc != RT_OK) return rc;
     p.scratch = (char*)c->scratch;
-    HIPCHK(hipMemsetAsync(c->counter, 0, sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(c->counter, 0, kStreams * kCtrStride * sizeof(uint32_t), st));
     hipLaunchKernelGGL(kern, dim3((uint32_t)nblocks), dim3(256), 0, st, p);
     HIPCHK(hipGetLastError());
     return RT_OK;

@@ -37,6 +37,14 @@ constexpr uint32_t kBlockShare = 24;
 // at any spp.  Without it the share bound took small launches to single pixels: a quarter of config B
 // (128 spp) then made 230 k claims, 2.5 ms of atomics for 1 ms of work (tools/multirank_check.sh).
 constexpr uint32_t kClaimSpp = 640;
+// The blocks past the first gridDim.x (one per workgroup, taken without an atomic) are dealt round-robin
+// to kStreams claim streams, stream s holding blocks gridDim.x + s + kStreams c (c = 0, 1, ...) behind its
+// own counter, kCtrStride words apart (256 B: separate lines and memory channels).  A workgroup claims
+// from stream blockIdx.x % kStreams (the XCD the hardware dispatches it to), and from the others once its
+// own runs dry, so the counters of a launch are not one word every CU hammers: the sky rows' cheap
+// pixels otherwise claimed faster than one word serves (~88 claims/us).
+constexpr uint32_t kStreams = 8;
+constexpr uint32_t kCtrStride = 64;
 
 // Block j of np items -> items [start, end); false past the last block.
 __device__ __forceinline__ bool guided_block(uint32_t np, uint32_t T, uint32_t G, uint32_t j, uint32_t& start,
@@ -78,6 +86,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ __attribute__((aligned(16))) T s_stage[4][3][64];   // finish_pixel: 64 positions' values per wave
     __shared__ IssueState s_is[4];
     __shared__ unsigned long long s_pool;   // the workgroup's pool of claimed items: next << 32 | end
+    __shared__ uint32_t s_dry;              // claim streams this workgroup found exhausted (bit s)
     __shared__ uint32_t q_sid[QW][QN];   // sid | slot << 29 (the pixel: s_slotpix[slot])
     __shared__ uint32_t s_slotpix[4][kSlots];   // the pixel of each open slot
     // ... and its work item (read at finish_pixel, not held in a VGPR)
@@ -112,7 +121,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         const auto& q = *cold_args<T>();
         uint32_t b0 = 0, b1 = 0;
         const bool got = guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, blockIdx.x, b0, b1);
-        if (threadIdx.x == 0) s_pool = got ? ((unsigned long long)b0 << 32) | b1 : 0ull;   // {next, end}; {0, 0}: empty
+        if (threadIdx.x == 0) {
+            s_pool = got ? ((unsigned long long)b0 << 32) | b1 : 0ull;   // {next, end}; {0, 0}: empty
+            s_dry = 0u;
+        }
     }
     __syncthreads();
     V3<T> o = mk(T(0), T(0), T(0)), d = o, c = o;
@@ -182,16 +194,20 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                             if (old == pv) { it = (uint32_t)(pv >> 32); break; }
                             pv = old;
                         }
-                        if (it == 0xFFFFFFFFu) {
-                            const uint32_t j = atomicAdd(q.counter, 1u) + gridDim.x;
-                            uint32_t b0 = 0, b1 = 0;
-                            if (guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, j, b0, b1)) {
-                                it = b0;
-                                if (b1 > b0 + 1u &&
-                                    atomicCAS(&s_pool, pv, ((unsigned long long)(b0 + 1u) << 32) | b1) != pv) {
-                                    nb = b0 + 1u;   // the pool was refilled meanwhile: keep the rest
-                                    ne = b1;
-                                }
+                        uint32_t b0 = 0, b1 = 0;
+                        bool claimed = false;
+                        for (uint32_t r = 0; it == 0xFFFFFFFFu && r < kStreams && !claimed; ++r) {
+                            const uint32_t s = (blockIdx.x + r) % kStreams;
+                            if ((__hip_atomic_load(&s_dry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> s) & 1u) continue;
+                            const uint32_t j = gridDim.x + s + kStreams * atomicAdd(q.counter + kCtrStride * s, 1u);
+                            claimed = guided_block(q.n_items, max(1u, kTMul * gridDim.x), q.blk_g, j, b0, b1);
+                            if (!claimed) atomicOr(&s_dry, 1u << s);   // blocks of a stream only grow in j
+                        }
+                        if (claimed) {
+                            it = b0;
+                            if (b1 > b0 + 1u && atomicCAS(&s_pool, pv, ((unsigned long long)(b0 + 1u) << 32) | b1) != pv) {
+                                nb = b0 + 1u;   // the pool was refilled meanwhile: keep the rest
+                                ne = b1;
                             }
                         }
                     }
