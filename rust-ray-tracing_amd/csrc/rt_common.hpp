@@ -137,10 +137,12 @@ constexpr uint32_t kFlagPinholeInternal = 0x80000000u;   // set by the host: def
 constexpr int kWavesF32 = 6;   // default min-waves-per-SIMD targets (measured sweep);
 constexpr int kWavesF64 = 4;   // RT_WAVES (read per launch) selects another for the live-path kernels
 constexpr int kWavesMegaF32 = 6;   // the mega-level kernels (config E; RT_WAVES=5 selects the W5 build)
-// fp32 launches below this many samples per resident W6 wave run at W5: W6's extra waves then split
-// the pixels thinner and the tail costs more than the occupancy gains (tools/waves_ab.py: an 8-way
-// shard of C, 21 600 samples per wave, is 6 % slower at W6; the 4-way shard, 43 200, 5.6 % faster)
-constexpr uint64_t kW6SamplesPerWave = 32768;
+// fp32 launches with fewer pixels than this per resident W6 wave run at W5: W6's extra waves then split
+// the pixels thinner and the tail costs more than the occupancy gains.  tools/waves_ab.py with the claim
+// streams (rt_trace.hpp), W6/W5 speed: C whole 1.058, 8-way shards (42 px per W6 wave) 1.032, 16-way
+// (21) 0.971; B 4-way (37.5) 1.056, 8-way (18.8) 0.966.  (Round 3's one claim counter put the 8-way
+// C shard on the other side.)
+constexpr uint64_t kW6PixelsPerWave = 24;
 // RT_WAVES=7 selects a 7-waves-per-SIMD fp32 live-path build (72 VGPRs; the LDS of 7 workgroups
 // just fits): +2 % on C and D, but it spills ~7 VGPRs around every sweep, and the scratch lines
 // (4 MB per XCD) push HBM writes from 23 to 41 B/sample, so the default stays at 6

@@ -529,7 +529,7 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     const int W = waves_env && atoi(waves_env) > 0 ? atoi(waves_env) : -1;
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
-    const bool big = (uint64_t)p.n_items * spp >= kW6SamplesPerWave * 24u * (uint64_t)c->n_cu;
+    const bool big = (uint64_t)p.n_items >= kW6PixelsPerWave * 24u * (uint64_t)c->n_cu;   // 24 W6 waves per CU
     void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, big)
                                     : pick_kernel<T, false>(flags, W, p.n_mg > 0, big);
     if (camq) {

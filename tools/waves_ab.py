@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Occupancy A/B on one GPU, same process: every fp32 launch shape the multi-GPU bench produces (config C
-whole and as each rank's shard of a 2/4/8-way split, one 8-way shard of D, 8- and 32-way shards of E),
+whole and as each rank's shard of a 2/4/8/16-way split, B's 4- and 8-way shards, one 8-way shard of D, 8- and 32-way shards of E),
 rendered at RT_WAVES=5 and 6 alternately (RT_WAVES is read per launch).  For an N-way split the slowest
 shard sets the frame time, so each line reports max over the ranks' kernel times.  Informational:
 the evidence for kWavesF32 / kWavesMegaF32."""
@@ -16,8 +16,8 @@ WAVES = sys.argv[1].split(",") if len(sys.argv) > 1 else ["5", "6"]
 REPS = 2
 lib = rt.load_library()
 r = rt.GpuRenderer(precision="f32", lib=lib)
-cases = [("C", 1, None), ("C", 2, None), ("C", 4, None), ("C", 8, None), ("D", 8, [0]), ("E", 8, [0]),
-         ("E", 32, [0, 16])]
+cases = [("C", 1, None), ("C", 2, None), ("C", 4, None), ("C", 8, None), ("C", 16, None), ("B", 4, None),
+         ("B", 8, None), ("D", 8, [0]), ("E", 8, [0]), ("E", 32, [0, 16])]
 for cfg, N, ranks in cases:
     W, H, n, spp, depth = rt.scenes.CONFIGS[cfg]
     flat = rt.scenes.config_scene(cfg).flatten()
