@@ -32,7 +32,7 @@ def launch(cfg, n, rank=0):
     cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
     tr = parallel.shard_range(W, H, n, rank)
     r.render_flat(depth, spp, flat, cam, tile_range=abi.RtTileRange(0, 8, 1, 0, W))   # warm-up (1 row)
-    buf = np.zeros((NW, 4), dtype=np.uint64)
+    buf = np.zeros((NW, 8), dtype=np.uint64)
     khz = ctypes.c_int()
     abi.check(lib, lib.rt_exp_timeline(r.ctx, buf.ctypes.data, NW, ctypes.byref(khz)))   # clear
     _, _, st, _ = r.render_flat(depth, spp, flat, cam, tile_range=tr)
@@ -58,3 +58,16 @@ for s in shapes:
           f"tail (end - drained) p50 {np.median(tail):.1f} p90 {np.percentile(tail, 90):.1f} max {tail.max():.1f} us | "
           f"iters p50 {np.median(w[:, 3]):.0f} | wave-time after drain {1 - dr.mean() / span:.3f}",
           flush=True)
+    # time per iteration by phase (median over waves): iterations 0-8, 8-32, 32-128, 128-drained
+    cp = [(w[:, 4 + j].astype(np.int64) - t0) * us for j in range(3)]
+    its = w[:, 3].astype(np.float64)
+    ph = [("0-8", start, cp[0], 8), ("8-32", cp[0], cp[1], 24), ("32-128", cp[1], cp[2], 96)]
+    out = []
+    for name, a, b, n_it in ph:
+        ok = w[:, 4 + [p_[0] for p_ in ph].index(name)] != 0
+        if ok.any():
+            out.append(f"{name} {np.median((b - a)[ok]) / n_it:.2f}")
+    ok = (w[:, 6] != 0) & (w[:, 1] != 0)
+    if ok.any():
+        out.append(f"128-drained {np.median(((dr - cp[2]) / np.maximum(its - 129, 1))[ok]):.2f}")
+    print("    us per iteration by phase (p50 over waves): " + ", ".join(out), flush=True)
