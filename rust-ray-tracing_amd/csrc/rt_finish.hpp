@@ -126,18 +126,6 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         if (lm) lmap[qq] = PScratch<T>::to16(smp);
         else sc.set_map(qq, smp);
     };
-    // Map init: no position holds a terminated sample's value yet (survivors and never-written
-    // positions read 0; positions [spp, P), the missing lanes of a partial last chunk, get their
-    // fixed value in the final reduction).  Two u16 entries per u32 store.
-    if (MODE == kModeV2) {
-        if (lm) {
-            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(lmap + qi) = 0xFFFFFFFFu;
-        } else if (sc.wide & 2u) {
-            for (uint32_t qi = lane; qi < P; qi += 64u) sc.set_map(qi, kNone);
-        } else {
-            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(sc.base + 2u * qi) = 0xFFFFFFFFu;
-        }
-    }
     // Bounce iterations the reference runs: K = min(depth, max e + 1).  The same pass builds the
     // histogram of the termination bounces below 64 (a sample terminated iff e < depth, and then
     // e < K); it is only used when K <= 64.
@@ -166,6 +154,23 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
         }
         K = min(depth, __builtin_amdgcn_readfirstlane(wave_max(me)) + 1u);
     }
+    // Sky pixels: K = 1 with depth > 1 means every sample hit the sky at bounce 0 (e = 0 < depth), so
+    // the replay is the identity (bounce 0 retires every position: lo = 0, and pold = pnew = i) and
+    // position q < spp holds white x sky(y_q) = sky(y_q).  No map, no replay, no colour reads (config C:
+    // the top third of the frame).
+    const bool sky_only = MODE == kModeV2 && depth > 1u && K == 1u;
+    // Map init: no position holds a terminated sample's value yet (survivors and never-written
+    // positions read 0; positions [spp, P), the missing lanes of a partial last chunk, get their
+    // fixed value in the final reduction).  Two u16 entries per u32 store.
+    if (MODE == kModeV2 && !sky_only) {
+        if (lm) {
+            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(lmap + qi) = 0xFFFFFFFFu;
+        } else if (sc.wide & 2u) {
+            for (uint32_t qi = lane; qi < P; qi += 64u) sc.set_map(qi, kNone);
+        } else {
+            for (uint32_t qi = 2u * lane; qi < P; qi += 128u) *(uint32_t*)(sc.base + 2u * qi) = 0xFFFFFFFFu;
+        }
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
     wave_mem_sync();
@@ -175,8 +180,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // k and moves to pnew = n_{k+1} + #{s' < s : e_s' == k} in the sorted copy (n_k = #{e >= k});
     // the retire rule then picks which of the two holds its value, and the position
     // map records the sample there (the value itself is formed in the final reduction).
-    bool replayed = false;
-    if (MODE == kModeV2 && K > 0u && K <= 64u) {
+    bool replayed = sky_only;
+    if (MODE == kModeV2 && K > 0u && K <= 64u && !sky_only) {
         replayed = true;
         const uint32_t H = hist[lane];   // lane k: #{e == k} over the pixel (pass 1)
         const uint32_t nn_l = spp - wave_scan_dpp(H);   // n_{k+1} = #{e > k} for k = lane
@@ -404,6 +409,9 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                         if (depth > 0u) { vr = s0.x; vg = s0.y; vb = s0.z; }
                         else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
                     }
+                } else if (MODE == kModeV2 && sky_only) {
+                    const V3<T> sk = sky(sc.y(s, qq));
+                    vr = sk.x; vg = sk.y; vb = sk.z;
                 } else if constexpr (MODE == kModeV2) {
                     uint32_t m;
                     if (lm) m = PScratch<T>::from16(lmap[qq]);
