@@ -111,12 +111,13 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
+// all_e0: every sample of the slot terminated at bounce 0 (trace_paths tracks it per slot).
 // The position map in LDS (live-path kernels without the mega level, P <= kLMapCap positions: config C's
 // 512 spp): the replay's scattered u16 writes, the map's initialisation and the reduction's reads stay
 // on the CU instead of going to HBM as partial lines.  Larger P uses the global map in PScratch.
 template <typename T, int MODE>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
-                                                 T (*stage)[64], uint16_t* lmap) {
+                                                 T (*stage)[64], uint16_t* lmap, bool all_e0 = false) {
     const auto& q = *cold_args<T>();
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t spp = q.spp, P = q.P, C = q.C, depth = q.depth;
@@ -131,13 +132,16 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     // e < K); it is only used when K <= 64.
     // (An incremental histogram kept by terminate as samples end, skipping this pass, measured -1.7 %
     // at config C fp32 and -1.0 % fp64: its per-termination LDS atomics cost more than the pass.)
+    // all_e0 (trace_paths: no sample of the slot terminated at a bounce e > 0): K = 1 without the pass.
     uint32_t K = 0;
-    const bool hist_on = MODE == kModeV2 && depth > 0u;
+    const bool known1 = MODE == kModeV2 && all_e0 && depth > 1u;
+    const bool hist_on = MODE == kModeV2 && depth > 0u && !known1;
     if (hist_on) {
         hist[lane] = 0u;
         __builtin_amdgcn_wave_barrier();
     }
-    if (depth > 0) {
+    if (known1) K = 1u;
+    else if (depth > 0) {
         uint32_t me = 0;
         for (uint32_t b = 0; b < spp; b += 512u) {
             uint32_t ev[8];

@@ -131,8 +131,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // the lane's sample and pixel slot in one VGPR, sid | slot << 29 (as in the camera queue: spp <= 2^20,
     // kSlots <= 8); the slot's pixel is read from s_slotpix where the scatter needs it
     uint32_t ss = 0, k = 0;
-    // lane s < kSlots: slot s's samples not yet terminated.  In a VGPR, not LDS: the LDS round trip sat
-    // on terminate's path every iteration (config E -4.6 %, C +-0 against this)
+    // lane s < kSlots: slot s's samples not yet terminated, | kSlotNZ once one of them terminated at a
+    // bounce e > 0 (so finish_pixel knows a sky pixel without reading its records).  In a VGPR, not LDS:
+    // the LDS round trip sat on terminate's path every iteration (config E -4.6 %, C +-0 against this)
+    constexpr uint32_t kSlotNZ = 0x80000000u;
     uint32_t slot_left = 0;
     auto sid_of = [](uint32_t v) -> uint32_t { return v & 0x1FFFFFFFu; };
     auto slot_of = [](uint32_t v) -> uint32_t { return v >> 29; };
@@ -265,21 +267,22 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             }
         }
         unsigned long long tm = __ballot(term);
+        const unsigned long long nzl = MODE == kModeV2 ? __ballot(term && e != 0u) : 0ull;
         bool synced = false;
         while (tm != 0ull) {
             const uint32_t s = __builtin_amdgcn_readlane(t_slot, __builtin_ctzll(tm));
             const unsigned long long m = __ballot(term && t_slot == s);
             tm &= ~m;
-            if (lane == s) slot_left -= (uint32_t)__popcll(m);
+            if (lane == s) slot_left = (slot_left - (uint32_t)__popcll(m)) | ((m & nzl) != 0ull ? kSlotNZ : 0u);
             const uint32_t left = __builtin_amdgcn_readlane(slot_left, s);
             // pixel complete: once per spp samples -- marked unlikely, so the register allocator
             // places any spill code here rather than in the sphere sweeps
-            if (__builtin_expect(left == 0u, 0)) {
+            if (__builtin_expect((left & ~kSlotNZ) == 0u, 0)) {
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
                 const uint32_t K = finish_pixel<T, MODE>(
                     wave_scratch<T>(wave), s, __builtin_amdgcn_readfirstlane(s_item[wave][s]), s_hist[wave], s_stage[wave],
-                    kLMap ? s_lmap[wave] : nullptr);
+                    kLMap ? s_lmap[wave] : nullptr, (left & kSlotNZ) == 0u);
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
