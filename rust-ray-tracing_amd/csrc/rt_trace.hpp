@@ -131,6 +131,20 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // the lane's sample and pixel slot in one VGPR, sid | slot << 29 (as in the camera queue: spp <= 2^20,
     // kSlots <= 8); the slot's pixel is read from s_slotpix where the scatter needs it
     uint32_t ss = 0, k = 0;
+    // The mega kernels keep ss in LDS, in this lane's word of the finish stage (s_stage, free outside
+    // finish_pixel; terminate saves and restores it around the call): at 80 VGPRs the allocator
+    // otherwise spills ss to scratch at every queue pop (config E's last hot-loop spill store).
+    constexpr bool kParkSS = MEGA;
+    uint32_t* const ssp = (uint32_t*)&s_stage[wave][0][0] + lane;
+    auto ss_get = [&]() -> uint32_t {
+        if constexpr (kParkSS) { asm volatile("" ::: "memory"); return *ssp; }
+        else return ss;
+    };
+    auto ss_set = [&](uint32_t v) {
+        if constexpr (kParkSS) *ssp = v;
+        else ss = v;
+    };
+    if constexpr (kParkSS) *ssp = 0u;
     // lane s < kSlots: slot s's samples not yet terminated, | kSlotNZ once one of them terminated at a
     // bounce e > 0 (so finish_pixel knows a sky pixel without reading its records).  In a VGPR, not LDS:
     // the LDS round trip sat on terminate's path every iteration (config E -4.6 %, C +-0 against this)
@@ -278,11 +292,16 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             // pixel complete: once per spp samples -- marked unlikely, so the register allocator
             // places any spill code here rather than in the sphere sweeps
             if (__builtin_expect((left & ~kSlotNZ) == 0u, 0)) {
+                const uint32_t ss_keep = kParkSS ? *ssp : 0u;   // finish_pixel overwrites the stage
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
                 const uint32_t K = finish_pixel<T, MODE>(
                     wave_scratch<T>(wave), s, __builtin_amdgcn_readfirstlane(s_item[wave][s]), s_hist[wave], s_stage[wave],
                     kLMap ? s_lmap[wave] : nullptr, (left & kSlotNZ) == 0u);
+                if constexpr (kParkSS) {
+                    __builtin_amdgcn_wave_barrier();
+                    *ssp = ss_keep;
+                }
                 if (lane == 0) wcount[wave][2] += K;
                 const uint32_t b = __builtin_amdgcn_readfirstlane(s_is[wave].busy);
                 if (lane == 0) s_is[wave].busy = b & ~(1u << s);
@@ -377,7 +396,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             const uint32_t r = lanes_below(freem);
             if (!live && r < take) {
                 const uint32_t e = (qhead + r) % QN;
-                ss = q_sid[wave][e];
+                ss_set(q_sid[wave][e]);
                 hit_i = q_hit[wave][e];
                 hit_t = q_t[wave][e];
                 const auto& q = *cold_args<T>();
@@ -396,21 +415,25 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             // ---- hand free lanes the next samples (opening new pixel slots as needed) ----
             uint32_t nsid = 0, nslot = 0;
             fresh = issue(__ballot(!live), nsid, nslot, npix, frow, fcol);
-            if (fresh) ss = nsid | (nslot << 29);
+            if (fresh) ss_set(nsid | (nslot << 29));
         }
         // ---- next rays: camera rays for fresh lanes, scattered rays for last iteration's hits ----
         if constexpr (kPark) unpark(o, d);
         if constexpr (kParkC) c = unpark_c();
         if (fresh || scat) {
-            const uint32_t pix = (!CAMQ && fresh) ? npix : s_slotpix[wave][slot_of(ss)];
-            next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid_of(ss), k, hit_i, hit_t, o, d, c);
+            const uint32_t ssv = ss_get();
+            const uint32_t pix = (!CAMQ && fresh) ? npix : s_slotpix[wave][slot_of(ssv)];
+            next_ray<T, SC>(CAMQ ? false : fresh, fcol, frow, pix, sid_of(ssv), k, hit_i, hit_t, o, d, c);
         }
         if constexpr (kPark) park(o, d);
         if constexpr (kParkC) park_c(c);
         if (fresh) {
             k = 0;
             live = true;
-            if (MODE == kModeV2) wave_scratch<T>(wave).y(slot_of(ss), sid_of(ss)) = d.y;   // primary y (quirk Q2)
+            if (MODE == kModeV2) {   // primary y (quirk Q2)
+                const uint32_t ssv = ss_get();
+                wave_scratch<T>(wave).y(slot_of(ssv), sid_of(ssv)) = d.y;
+            }
         } else if (scat) {
             k += 1u;
         }
@@ -432,7 +455,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             if (MODE != kModeV2) { V3<T> po, pd; unpark(po, pd); d = pd; }   // the own-value modes read d
         }
         if constexpr (kParkC) c = unpark_c();
-        terminate(term, skyhit, skyhit ? k : depth, slot_of(ss), sid_of(ss), c, d);
+        {
+            const uint32_t ssv = ss_get();
+            terminate(term, skyhit, skyhit ? k : depth, slot_of(ssv), sid_of(ssv), c, d);
+        }
         live = live && !term;
     }
     if (lane == 0) {
