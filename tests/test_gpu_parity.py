@@ -88,6 +88,17 @@ def test_empty_scene(renderer):
     assert np.all((lin > 0.5) & (lin <= 1.0)) and st.ray_segments == 40 * 30 * 8
 
 
+@pytest.mark.parametrize("depth", [2, 50])
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+@pytest.mark.parametrize("spp", [1, 6, 100, 512])
+def test_sky_pixels(renderer, spp, flags, depth):
+    """Every sample escapes at bounce 0, so every pixel takes finish_pixel's sky path (no position map,
+    no replay, no colour reads; the slot's bounce flag stays clear): partial chunks (1, 6), quirk Q3's
+    other buffer (100), config C's spp (512), both precisions."""
+    flat = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((0.5, 0.5, 0.5))])
+    assert_parity(renderer, flat, cam_for(16, 9), depth, spp, flags)
+
+
 def test_large_spp(renderer, scene_100):
     assert_parity(renderer, scene_100, cam_for(8, 6), 50, 1024, 0)            # P = 1024, fp64
     assert_parity(renderer, scene_100, cam_for(8, 6), 50, 2048, abi.RT_FLAG_F32)  # two slots per thread
