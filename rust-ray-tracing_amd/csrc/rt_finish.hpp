@@ -109,6 +109,93 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
     return v;
 }
 
+// The final reduction in the reference's order (ray_tracing.rs:499-502, color.rs:226-232): per lane l of
+// PackedColor<4>, chunks j = 0..C-1 from +0.0, over the values vals(q, r, g, b) forms for positions
+// q < P.  All 64 lanes form the values of 64 positions at a time into LDS (stage, transposed); lanes
+// ch * 4 + l then add theirs in order, the 12 running sums kept in LDS (hist) between batches: a short
+// live range keeps this loop from raising the kernel's register peak.  Returns lane ch * 4 + l's sum.
+template <typename T, typename F>
+__device__ __forceinline__ T reduce_positions(uint32_t P, uint32_t* hist, T (*stage)[64], F&& vals) {
+    const uint32_t lane = threadIdx.x & 63u;
+    T* accl = (T*)hist;
+    if (lane < 12u) accl[lane] = T(0.0);
+    for (uint32_t qb = 0; qb < P; qb += 64u) {
+        const uint32_t qq = qb + lane;
+        T vr = T(0.0), vg = T(0.0), vb = T(0.0);
+        if (qq < P) vals(qq, vr, vg, vb);
+        // transposed: lane (ch, l) finds its 16 values (positions qb + 4u + l) contiguous
+        const uint32_t si = 16u * (lane & 3u) + (lane >> 2);
+        stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 12u) {
+            const uint32_t nu = min(16u, (P - qb) / 4u);   // wave-uniform; 16 except a short last batch
+            const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
+            T a = accl[lane];
+            if (nu == 16u) {   // a whole batch: plain adds (the guarded form costs a compare and a select each)
+#pragma unroll
+                for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
+                    T v[4];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
+#pragma unroll
+                    for (uint32_t u = 0; u < 4u; ++u) a = a + v[u];
+                }
+            } else {
+                for (uint32_t u = 0; u < nu; ++u) a = a + sv[u];
+            }
+            accl[lane] = a;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return lane < 12u ? accl[lane] : T(0.0);
+}
+
+// The pixel's value: PackedColor::sum of the 4 lanes' sums (or the scalar mode's average), / spp
+// (renderer.rs:161), Color::to_u8_array's assert and bytes (color.rs:54-64).
+template <typename T, int MODE>
+__device__ __forceinline__ void write_pixel(T acc, uint32_t item) {
+    const auto& q = *cold_args<T>();
+    const uint32_t lane = threadIdx.x & 63u;
+    const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
+            s3 = __shfl(acc, (int)((lane + 3) & 63u));
+    const bool writer = MODE == kModeScalar ? lane < 3u : (lane < 12u && (lane & 3u) == 0u);
+    if (writer) {
+        const uint32_t ch = MODE == kModeScalar ? lane : lane >> 2;
+        const T tot = MODE == kModeScalar ? acc : (((T(0.0) + acc) + s1) + s2) + s3;
+        const T v = tot / (T)q.spp;                                 // renderer.rs:161
+        if (!(v <= T(2.0))) atomicOr(q.err, 1u);                    // color.rs:55-57 assert
+        if (q.rgb) q.rgb[(size_t)item * 3 + ch] = q8(v);
+        if (q.lin) q.lin[(size_t)item * 3 + ch] = (double)v;
+    }
+}
+
+// A sky pixel finished without tracing (trace_paths, camera batches: a pixel whose camera candidate
+// list is empty, so none of its primary rays can hit a sphere and every sample escapes at bounce 0;
+// depth > 1).  As finish_pixel's sky path (the replay is the identity, position q < spp holds
+// sky(y_q)), with y_q the primary direction's y that Camera::get_ray (ray_tracing.rs:77-89) gives
+// sample q, computed here exactly as the camera batches compute it; positions past spp hold sky(0).
+template <typename T>
+__device__ __forceinline__ void finish_sky_direct(uint32_t item, uint32_t col, uint32_t row, uint32_t pix,
+                                                  uint32_t* hist, T (*stage)[64]) {
+    const auto& q = *cold_args<T>();
+    const uint32_t spp = q.spp;
+    const V3<T> s0 = sky(T(0.0));
+    const T acc = reduce_positions<T>(q.P, hist, stage, [&](uint32_t qq, T& vr, T& vg, T& vb) {
+        if (qq >= spp) { vr = s0.x; vg = s0.y; vb = s0.z; return; }
+        const auto& qc = *cold_args<T>();
+        const U4 r = philox(qq, pix, 0u, 0u, qc.k0, qc.k1);
+        const T s1 = div_dim((T)col + u01a(r, T(0)), qc.W, qc.rW);
+        const T s2 = div_dim((T)row + u01b(r, T(0)), qc.H, qc.rH);
+        const V3<T> vu = mk(qc.vu[0], qc.vu[1], qc.vu[2]), vv = mk(qc.vv[0], qc.vv[1], qc.vv[2]);
+        const V3<T> pc = add(mk(qc.ulc[0], qc.ulc[1], qc.ulc[2]), add(mul(vu, s1), mul(vv, s2)));
+        const V3<T> sk = sky(unit(sub(pc, mk(qc.center[0], qc.center[1], qc.center[2]))).y);
+        vr = sk.x; vg = sk.y; vb = sk.z;
+    });
+    write_pixel<T, kModeV2>(acc, item);
+}
+
 // Replay pixel slot s's positions from its records, apply the retire rule, reduce, write the
 // pixel (whole wave; returns the number of bounce iterations the reference runs for the pixel).
 // all_e0: every sample of the slot terminated at bounce 0 (trace_paths tracks it per slot).
@@ -388,14 +475,8 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     } else {
         const V3<T> s0 = sky(T(0.0));
         const bool white0 = depth == 0u && q.s_sel == 0u;
-        // the 12 running sums live in LDS (the free histogram) between batches: a short live range
-        // keeps this loop from raising the kernel's register peak
-        T* accl = (T*)hist;
-        if (lane < 12u) accl[lane] = T(0.0);
-        for (uint32_t qb = 0; qb < P; qb += 64u) {
-            const uint32_t qq = qb + lane;
-            T vr = T(0.0), vg = T(0.0), vb = T(0.0);
-            if (qq < P && MODE == kModeV3) {
+        acc = reduce_positions<T>(P, hist, stage, [&](uint32_t qq, T& vr, T& vg, T& vb) {
+            if (MODE == kModeV3) {
                 // the sample at slot qq: its own value; a missing lane (white, hit_sky at bounce 0
                 // with a zero direction) adds sky(0), or white when no bounce ran (:611-619)
                 const uint32_t m = ((const uint32_t*)sc.base)[qq];
@@ -407,71 +488,33 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 } else {
                     vr = T(1.0); vg = T(1.0); vb = T(1.0);
                 }
-            } else if (qq < P) {
-                if (qq >= spp) {
-                    if (MODE == kModeV2) {
-                        if (depth > 0u) { vr = s0.x; vg = s0.y; vb = s0.z; }
-                        else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
-                    }
-                } else if (MODE == kModeV2 && sky_only) {
+            } else if (qq >= spp) {
+                if (MODE == kModeV2) {
+                    if (depth > 0u) { vr = s0.x; vg = s0.y; vb = s0.z; }
+                    else if (white0) { vr = T(1.0); vg = T(1.0); vb = T(1.0); }
+                }
+            } else if (MODE == kModeV2 && sky_only) {
+                const V3<T> sk = sky(sc.y(s, qq));
+                vr = sk.x; vg = sk.y; vb = sk.z;
+            } else if constexpr (MODE == kModeV2) {
+                uint32_t m;
+                if (lm) m = PScratch<T>::from16(lmap[qq]);
+                else m = sc.map(qq);
+                if (m != kNone) {
+                    // a bounce-0 sky hit (kWhite) wrote no record: white x sky.  Branch-free (the
+                    // record slot is read anyway and replaced by white: a branch cost 0.8 % at C)
+                    const bool wh = (m & PScratch<T>::kWhite) != 0u;
+                    const C3<T> cm = sc.c(s, m & ~PScratch<T>::kWhite);
                     const V3<T> sk = sky(sc.y(s, qq));
-                    vr = sk.x; vg = sk.y; vb = sk.z;
-                } else if constexpr (MODE == kModeV2) {
-                    uint32_t m;
-                    if (lm) m = PScratch<T>::from16(lmap[qq]);
-                    else m = sc.map(qq);
-                    if (m != kNone) {
-                        // a bounce-0 sky hit (kWhite) wrote no record: white x sky.  Branch-free (the
-                        // record slot is read anyway and replaced by white: a branch cost 0.8 % at C)
-                        const bool wh = (m & PScratch<T>::kWhite) != 0u;
-                        const C3<T> cm = sc.c(s, m & ~PScratch<T>::kWhite);
-                        const V3<T> sk = sky(sc.y(s, qq));
-                        vr = (wh ? T(1.0) : cm.x) * sk.x; vg = (wh ? T(1.0) : cm.y) * sk.y; vb = (wh ? T(1.0) : cm.z) * sk.z;
-                    }
-                } else {
-                    const C3<T> cm = sc.c(s, qq);
-                    vr = cm.x; vg = cm.y; vb = cm.z;
+                    vr = (wh ? T(1.0) : cm.x) * sk.x; vg = (wh ? T(1.0) : cm.y) * sk.y; vb = (wh ? T(1.0) : cm.z) * sk.z;
                 }
+            } else {
+                const C3<T> cm = sc.c(s, qq);
+                vr = cm.x; vg = cm.y; vb = cm.z;
             }
-            // transposed: lane (ch, l) finds its 16 values (positions qb + 4u + l) contiguous
-            const uint32_t si = 16u * (lane & 3u) + (lane >> 2);
-            stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            __builtin_amdgcn_wave_barrier();
-            if (lane < 12u) {
-                const uint32_t nu = min(16u, (P - qb) / 4u);   // wave-uniform; 16 except a short last batch
-                const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
-                T a = accl[lane];
-                if (nu == 16u) {   // a whole batch: plain adds (the guarded form costs a compare and a select each)
-#pragma unroll
-                    for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
-                        T v[4];
-#pragma unroll
-                        for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
-#pragma unroll
-                        for (uint32_t u = 0; u < 4u; ++u) a = a + v[u];
-                    }
-                } else {
-                    for (uint32_t u = 0; u < nu; ++u) a = a + sv[u];
-                }
-                accl[lane] = a;
-            }
-            __builtin_amdgcn_wave_barrier();
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        if (lane < 12u) acc = accl[lane];
+        });
     }
-    const T s1 = __shfl(acc, (int)((lane + 1) & 63u)), s2 = __shfl(acc, (int)((lane + 2) & 63u)),
-            s3 = __shfl(acc, (int)((lane + 3) & 63u));
-    const bool writer = MODE == kModeScalar ? lane < 3u : (lane < 12u && (lane & 3u) == 0u);
-    if (writer) {
-        const uint32_t ch = MODE == kModeScalar ? lane : lane >> 2;
-        const T tot = MODE == kModeScalar ? acc : (((T(0.0) + acc) + s1) + s2) + s3;
-        const T v = tot / (T)spp;                                   // renderer.rs:161
-        if (!(v <= T(2.0))) atomicOr(q.err, 1u);                    // color.rs:55-57 assert
-        if (q.rgb) q.rgb[(size_t)item * 3 + ch] = q8(v);
-        if (q.lin) q.lin[(size_t)item * 3 + ch] = (double)v;
-    }
+    write_pixel<T, MODE>(acc, item);
     return K;
 }
 

@@ -178,6 +178,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
 
     // Hand the lanes of `want` new samples in rank order, opening pixel slots as needed; returns
     // true in the lanes that got one.
+    // Camera batches on the live path: pixels whose camera candidate list is empty finish at claim time
+    constexpr bool kDirectSky = CAMQ && MODE == kModeV2;
     auto issue = [&](unsigned long long want, uint32_t& i_sid, uint32_t& i_slot, uint32_t& i_pix,
                      uint32_t& i_row, uint32_t& i_col) -> bool {
         const uint32_t spp = cold_args<T>()->spp;
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         bool drained = __builtin_amdgcn_readfirstlane(s_is[wave].drained) != 0u;
         uint32_t blk_next = __builtin_amdgcn_readfirstlane(s_is[wave].blk_next);
         uint32_t blk_end = __builtin_amdgcn_readfirstlane(s_is[wave].blk_end);
-        uint32_t opened = 0;
+        uint32_t opened = 0, listed = 0;
         while (want != 0ull && !drained) {
             if (cur_next == spp) {
                 const uint32_t avail = ~busy & ((1u << kSlots) - 1u);
@@ -238,6 +240,27 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 cur_row = q.row_begin + ri * q.row_step;
                 cur_col = q.col_begin + ci;
                 cur_pix = cur_row * q.W + cur_col;
+                if constexpr (kDirectSky) {
+                    if (cold_args<T>()->depth > 1u) {
+                        // the pixel's camera candidate list now, not at its slot's first batch: an empty
+                        // one means no primary ray of the pixel can hit a sphere, so every sample escapes
+                        // at bounce 0 and the pixel is finished here without tracing (finish_sky_direct);
+                        // its slot stays free
+                        const uint32_t nl = pixel_list<T, MEGA>(cur_col, cur_row, s_clist[wave][s]);
+                        if (nl == 0u) {
+                            const uint32_t ss_keep = kParkSS ? *ssp : 0u;   // the stage is overwritten
+                            finish_sky_direct<T>(item, cur_col, cur_row, cur_pix, s_hist[wave], s_stage[wave]);
+                            if constexpr (kParkSS) {
+                                __builtin_amdgcn_wave_barrier();
+                                *ssp = ss_keep;
+                            }
+                            // its spp primary segments and one bounce iteration, as traced
+                            if (lane == 0) { wcount[wave][0] += spp; wcount[wave][1] += spp; wcount[wave][2] += 1u; }
+                            continue;
+                        }
+                        listed |= 1u << s;
+                    }
+                }
                 if (lane == 0) { s_slotpix[wave][s] = cur_pix; s_item[wave][s] = item; }
                 if (lane == s) slot_left = spp;
                 busy |= 1u << s;
@@ -257,7 +280,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
             s_is[wave].busy = busy; s_is[wave].cur = cur; s_is[wave].cur_next = cur_next; s_is[wave].cur_pix = cur_pix;
             s_is[wave].cur_row = cur_row; s_is[wave].cur_col = cur_col; s_is[wave].drained = drained ? 1u : 0u;
             s_is[wave].blk_next = blk_next; s_is[wave].blk_end = blk_end;
-            if (CAMQ) s_is[wave].need |= opened;
+            if (CAMQ) s_is[wave].need |= opened & ~listed;
         }
         return got;
     };
