@@ -99,8 +99,10 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // across the sphere sweeps and the camera batches and re-read right before the scatter, instead
     // of being held in VGPRs (the allocator otherwise spills them to scratch memory around the sweep).
     constexpr bool kPark = (sizeof(T) == 4 && W >= 6) || kF64Park;
-    // the mega-level kernels park the path colour as well (their four-level sweep holds more state)
-    constexpr bool kParkC = kPark && MEGA;
+    // the mega-level kernels park the path colour as well (their four-level sweep holds more state), and
+    // so does fp32 at W6 since issue() finishes sky pixels (it pushed the colour into scratch spills
+    // around the scatter; parked: C +0.9 % same-box, LDS 26.8 of 27.3 KB per workgroup)
+    constexpr bool kParkC = kPark && (MEGA || (sizeof(T) == 4 && W == 6));
     __shared__ T s_park[kPark ? 4 : 1][kParkC ? 9 : 6][64];
     // finish_pixel's position map (P <= kLMapCap) in LDS: the fp64 live-path kernels without the mega level
     // (fp64 C +1.1 % same-box).  fp32 lost 7 % with it (the extra finish_pixel code pushed 5 more spills
