@@ -449,7 +449,7 @@ def main():
                                       "x_fp32_peak": bf / launch_s / 1e12 / PEAK_TF["f32"]},
             },
             "ray_segments_per_sample": st.ray_segments / max(1.0, per_rank[rank][6] * spp * args.steps),
-            "lane_utilisation": st.ray_segments / max(1, st.lane_slots),
+            "lane_utilisation": abi.lane_utilisation(st),
             "bounces_per_pixel": st.bounce_iters / max(1, st.pixels),
             "range_error": rc == abi.RT_ERR_RANGE,
             "per_rank": per_rank,

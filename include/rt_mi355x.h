@@ -85,7 +85,7 @@ typedef struct rt_stats {
     uint64_t samples;        /* pixels * spp */
     uint64_t ray_segments;   /* enabled rays traced, summed over bounces (ray_tracing.rs:396-401) */
     uint64_t lane_slots;     /* SIMD lanes issued for those traces (64 per wave-bounce);
-                                ray_segments / lane_slots = lane utilisation */
+                                (ray_segments - direct_sky_samples) / lane_slots = lane utilisation */
     uint64_t bounce_iters;   /* bounce-loop iterations executed, summed over pixels */
     /* Executed work of the culls and exact tests, in wave-level tests (each runs all 64 lanes of a
      * wave); DESIGN.md §5 turns them into executed FLOP for the roofline:
@@ -97,7 +97,26 @@ typedef struct rt_stats {
      *   camera_exact_tests  camera sweep, one sphere each from the camera-origin table: 8 FLOP per
      *                       lane in the render's precision */
     uint64_t box_groups, filter_groups, exact_tests, cone_tests, camera_exact_tests;
+    /* Samples of pixels finished when they are claimed, without tracing: a pinhole camera's pixel
+     * whose camera candidate list is empty (no primary ray of the pixel can hit a sphere, so every
+     * sample escapes at bounce 0).  Their primary segments are in ray_segments (the reference traces
+     * them, ray_tracing.rs:396-401) but occupy no SIMD lane, so they are not in lane_slots. */
+    uint64_t direct_sky_samples;
+    /* The kernel the last collected render ran (RT_KERNEL_* fields below; 0 = none) and how many of
+     * its 4-wave workgroups were resident per CU (hipOccupancyMaxActiveBlocksPerMultiprocessor): equal
+     * to the kernel's waves-per-SIMD target unless LDS or registers cut its occupancy. */
+    uint32_t kernel_id;
+    uint32_t kernel_wg_per_cu;
 } rt_stats;
+
+/* rt_stats.kernel_id: trace_paths<T, W, ROOT2, MODE, CAMQ, MEGA> of rt_kernel.hip, one bit field each.
+ * Bit 15 is set for any kernel, so 0 means "no render collected". */
+#define RT_KERNEL_F64(id) ((id) & 1u)            /* T = double (else float) */
+#define RT_KERNEL_WAVES(id) (((id) >> 1) & 7u)   /* W: waves per SIMD the register allocation targets */
+#define RT_KERNEL_ROOT2(id) (((id) >> 4) & 1u)   /* quirk Q1 off */
+#define RT_KERNEL_MODE(id) (((id) >> 5) & 3u)    /* 0 live path, 1 vectorized, 2 scalar, 3 vectorized3 */
+#define RT_KERNEL_CAMQ(id) (((id) >> 7) & 1u)    /* pinhole camera batches */
+#define RT_KERNEL_MEGA(id) (((id) >> 8) & 1u)    /* four-level sweep (mega boxes; scenes of > 8 super groups) */
 
 /* ---- flags ---- */
 #define RT_FLAG_F32 0x1u     /* compute in fp32 (default: fp64, the reference's arithmetic) */

@@ -147,7 +147,7 @@ constexpr uint64_t kW6PixelsPerWave = 24;
 // just fits): +2 % on C and D, but it spills ~7 VGPRs around every sweep, and the scratch lines
 // (4 MB per XCD) push HBM writes from 23 to 41 B/sample, so the default stays at 6
 template <typename T> constexpr int kWavesModes = sizeof(T) == 4 ? 6 : 4;   // ROOT2 and semantics modes
-constexpr int kSegStride = 16;  // u64 per shard (128 B)
+constexpr int kSegStride = 32;  // u64 per shard (256 B)
 constexpr float kFilterMargin = 48.0f * 0x1.0p-24f;   // general-sweep filter margin factor (nearest_hit)
 constexpr double kExactRatio = 8.0;  // spheres with |c|_1 + r > kExactRatio x the median are "always exact"
 
@@ -163,7 +163,8 @@ enum WorkCounter : uint32_t {
     kNWork = 5,
 };
 constexpr int kWorkSlot = 11;   // shard slots 11..15 (kstats uses 3..10)
-static_assert(kWorkSlot + kNWork <= kSegStride, "work counters past the shard's line");
+constexpr int kDirectSkySlot = 16;   // samples of pixels finished at claim time (rt_stats.direct_sky_samples)
+static_assert(kWorkSlot + kNWork <= kDirectSkySlot && kDirectSkySlot < kSegStride, "counters past the shard's slots");
 // u64: a wave of a persistent launch can run billions of tests (config E: ~1.3M filter groups per
 // wave; spp up to 2^20 on a 4K frame is ~3000x that), past a u32.
 __shared__ unsigned long long g_work[4][kNWork];

@@ -106,6 +106,7 @@ struct rt_context {
     uint64_t scene_gen = 0;
     struct CamKey { bool valid = false; uint64_t gen = 0; double center[3] = {0, 0, 0}; uint32_t scalar = 0, off = 0; };
     CamKey camkey[2];   // [0] fp32 tables, [1] fp64
+    uint32_t last_kernel_id = 0, last_wg_per_cu = 0;   // rt_stats.kernel_id / kernel_wg_per_cu of the last launch
 };
 
 extern "C" const char* rt_last_error(void) { return g_err.c_str(); }
@@ -397,33 +398,47 @@ static int ensure_scratch(rt_context* c, size_t bytes, hipStream_t st);
 // The kernel instantiation for (flags, waves-per-SIMD target, camera batches, mega level).  W < 0:
 // the defaults (RT_WAVES unset).  The mega level (scenes with more than 8 super groups) has its own
 // live-path kernels (fp32 at 5 or 6 waves, default 6; fp64 at 4); at other W such scenes are swept
-// from the super boxes (the same result, more box tests).
+// from the super boxes (the same result, more box tests).  id: rt_stats.kernel_id (rt_mi355x.h).
+template <typename T> struct KernelPick {
+    void (*fn)(KParams<T>);
+    uint32_t id;
+    int W;
+};
+template <typename T, int W, bool ROOT2, int MODE, bool CAMQ, bool MEGA = false>
+static KernelPick<T> kp() {
+    const uint32_t id = 0x8000u | (sizeof(T) == 8 ? 1u : 0u) | ((uint32_t)W << 1) | (ROOT2 ? 1u << 4 : 0u) |
+                        ((uint32_t)MODE << 5) | (CAMQ ? 1u << 7 : 0u) | (MEGA ? 1u << 8 : 0u);
+    return KernelPick<T>{trace_paths<T, W, ROOT2, MODE, CAMQ, MEGA>, id, W};
+}
 template <typename T, bool CAMQ>
-static void (*pick_kernel(uint32_t flags, int W, bool mega, bool big))(KParams<T>) {
+static KernelPick<T> pick_kernel(uint32_t flags, int W, bool mega, bool big) {
     const bool r2 = (flags & RT_FLAG_ROOT2) != 0u;
     constexpr bool F32 = sizeof(T) == 4;
     constexpr int WM = kWavesModes<T>;
-    if (flags & RT_FLAG_MODE_SCALAR) return trace_paths<T, WM, false, kModeScalar, CAMQ>;
+    if (flags & RT_FLAG_MODE_SCALAR) return kp<T, WM, false, kModeScalar, CAMQ>();
     if (flags & RT_FLAG_MODE_VECTORIZED3)
-        return r2 ? trace_paths<T, WM, true, kModeV3, CAMQ> : trace_paths<T, WM, false, kModeV3, CAMQ>;
+        return r2 ? kp<T, WM, true, kModeV3, CAMQ>() : kp<T, WM, false, kModeV3, CAMQ>();
     if (flags & RT_FLAG_MODE_VECTORIZED)
-        return r2 ? trace_paths<T, WM, true, kModeV1, CAMQ> : trace_paths<T, WM, false, kModeV1, CAMQ>;
-    if (r2) return trace_paths<T, WM, true, kModeV2, CAMQ>;
+        return r2 ? kp<T, WM, true, kModeV1, CAMQ>() : kp<T, WM, false, kModeV1, CAMQ>();
+    if (r2) return kp<T, WM, true, kModeV2, CAMQ>();
     if (mega) {
         const int Wm = W < 0 ? (F32 ? (big ? kWavesMegaF32 : 5) : kWavesF64) : W;
         if constexpr (F32) {
-            if (Wm == 5) return trace_paths<T, 5, false, kModeV2, CAMQ, true>;
-            if (Wm == 6) return trace_paths<T, 6, false, kModeV2, CAMQ, true>;
+            if (Wm == 5) return kp<T, 5, false, kModeV2, CAMQ, true>();
+            if (Wm == 6) return kp<T, 6, false, kModeV2, CAMQ, true>();
         } else {
-            if (Wm == 4) return trace_paths<T, 4, false, kModeV2, CAMQ, true>;
+            if (Wm == 4) return kp<T, 4, false, kModeV2, CAMQ, true>();
         }
     }
     if (W < 0) W = F32 ? (big ? kWavesF32 : 5) : kWavesF64;
+    // RT_WAVES above what the kernel's LDS allows is clamped: fp32 6 (round 2's W7 build lost its
+    // seventh workgroup to the camera lists and the parking: 5 resident), fp64 5 (its W6 build: 3)
     if constexpr (F32) {
-        if (W >= 7) return trace_paths<T, 7, false, kModeV2, CAMQ>;
+        return W >= 6 ? kp<T, 6, false, kModeV2, CAMQ>() : W >= 5 ? kp<T, 5, false, kModeV2, CAMQ>()
+                                                         : kp<T, 4, false, kModeV2, CAMQ>();
+    } else {
+        return W >= 5 ? kp<T, 5, false, kModeV2, CAMQ>() : kp<T, 4, false, kModeV2, CAMQ>();
     }
-    return W >= 6 ? trace_paths<T, 6, false, kModeV2, CAMQ> : W >= 5 ? trace_paths<T, 5, false, kModeV2, CAMQ>
-                                                           : trace_paths<T, 4, false, kModeV2, CAMQ>;
 }
 
 template <typename T>
@@ -530,8 +545,9 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // Camera batches + camera-origin table when every primary ray starts at the centre.
     const bool camq = (p.flags & kFlagPinholeInternal) && depth >= 1u;
     const bool big = (uint64_t)p.n_items >= kW6PixelsPerWave * 24u * (uint64_t)c->n_cu;   // 24 W6 waves per CU
-    void (*kern)(KParams<T>) = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, big)
+    const KernelPick<T> pick = camq ? pick_kernel<T, true>(flags, W, p.n_mg > 0, big)
                                     : pick_kernel<T, false>(flags, W, p.n_mg > 0, big);
+    void (*kern)(KParams<T>) = pick.fn;
     if (camq) {
         p.camsph = (const T*)(f64 ? c->cam64 : c->cam32);
         p.camf = (const float*)(f64 ? c->camf64 : c->camf32);
@@ -565,6 +581,16 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     int per_cu = 0;
     HIPCHK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, 256, 0));
     if (per_cu < 1) per_cu = 1;
+    // 4-wave workgroups: W waves per SIMD is W workgroups per CU.  Fewer means the kernel's LDS (or
+    // registers) cut its occupancy below the target it was built for (kParkC takes fp32 W6 to 26.8 of the
+    // 27.3 KB six workgroups allow): an error, in every build kind, so that neither the product nor an
+    // A/B build is ever measured at an occupancy other than the one it names (rt_stats reports both).
+    c->last_kernel_id = pick.id;
+    c->last_wg_per_cu = (uint32_t)per_cu;
+    if (per_cu < pick.W)
+        return fail(RT_ERR_UNSUPPORTED, std::string(RT_BUILD_KIND) + " build: " + std::to_string(per_cu) +
+                                            " workgroups per CU resident, kernel built for " + std::to_string(pick.W) +
+                                            " (its LDS or registers grew past the occupancy target)");
     uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
     const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
     if (nblocks > need) nblocks = need;
@@ -660,7 +686,7 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
     if (c->have_first) HIPCHK(hipEventElapsedTime(&ms, c->ev_first, c->ev_last));
     HIPCHK(hipMemset(c->segs, 0, segs.size() * sizeof(unsigned long long)));
     HIPCHK(hipMemset(c->err, 0, 16));
-    uint64_t total = 0, slots = 0, iters = 0, kst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, work[kNWork] = {};
+    uint64_t total = 0, slots = 0, iters = 0, dsky = 0, kst[8] = {0, 0, 0, 0, 0, 0, 0, 0}, work[kNWork] = {};
     for (int i = 0; i < kSegShards; ++i)
         for (int j = 0; j < 8; ++j) kst[j] += segs[(size_t)i * kSegStride + 3 + j];
     if (kst[0] | kst[1] | kst[2] | kst[3])   // instrumented build (make kstats) only
@@ -673,6 +699,7 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
         total += segs[(size_t)i * kSegStride];
         slots += segs[(size_t)i * kSegStride + 1];
         iters += segs[(size_t)i * kSegStride + 2];
+        dsky += segs[(size_t)i * kSegStride + kDirectSkySlot];
         for (uint32_t j = 0; j < kNWork; ++j) work[j] += segs[(size_t)i * kSegStride + kWorkSlot + j];
     }
     if (out) {
@@ -689,9 +716,13 @@ extern "C" int rt_context_collect(rt_context* c, void* stream, rt_stats* out) {
         out->exact_tests = work[kWExact];
         out->cone_tests = work[kWCone];
         out->camera_exact_tests = work[kWCExact];
+        out->direct_sky_samples = dsky;
+        out->kernel_id = c->last_kernel_id;
+        out->kernel_wg_per_cu = c->last_wg_per_cu;
     }
     c->have_first = false;
     c->pixels = c->samples = 0;
+    c->last_kernel_id = c->last_wg_per_cu = 0;
     if (err) return fail(RT_ERR_RANGE, "a pixel channel exceeded 2.0 (Color::to_u8_array would panic, color.rs:55-57)");
     return RT_OK;
 }

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     // workgroup
     constexpr bool kF64Park = sizeof(T) == 8 && W >= 5;
     constexpr uint32_t QW = CAMQ ? 4 : 1, QN = CAMQ ? (kF64Park ? 64u : kQCap) : 1;
-    __shared__ unsigned long long wcount[4][3];
+    __shared__ unsigned long long wcount[4][4];   // segments, lane slots, bounce iterations, direct sky samples
     // 8-byte aligned: finish_pixel keeps its 12 running sums (T, fp64 too) in this array
     __shared__ __attribute__((aligned(16))) uint32_t s_hist[4][64];
     __shared__ __attribute__((aligned(16))) T s_stage[4][3][64];   // finish_pixel: 64 positions' values per wave
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ __attribute__((aligned(16))) uint16_t s_lmap[kLMap ? 4 : 1][kLMap ? kLMapCap : 2];
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; }
+    if (lane == 0) { wcount[wave][0] = 0; wcount[wave][1] = 0; wcount[wave][2] = 0; wcount[wave][3] = 0; }
     if (lane < kNWork) g_work[wave][lane] = 0ull;
 #ifdef RT_KSTATS
     if (lane < 8) g_kst[wave][lane] = 0;
@@ -256,8 +256,8 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                                 __builtin_amdgcn_wave_barrier();
                                 *ssp = ss_keep;
                             }
-                            // its spp primary segments and one bounce iteration, as traced
-                            if (lane == 0) { wcount[wave][0] += spp; wcount[wave][1] += spp; wcount[wave][2] += 1u; }
+                            // its spp primary segments and one bounce iteration, as traced; no lane held them
+                            if (lane == 0) { wcount[wave][0] += spp; wcount[wave][3] += spp; wcount[wave][2] += 1u; }
                             continue;
                         }
                         listed |= 1u << s;
@@ -493,6 +493,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         atomicAdd(cc + 0, wcount[wave][0]);
         atomicAdd(cc + 1, wcount[wave][1]);
         atomicAdd(cc + 2, wcount[wave][2]);
+        if (wcount[wave][3]) atomicAdd(cc + kDirectSkySlot, wcount[wave][3]);
         for (uint32_t i = 0; i < kNWork; ++i) atomicAdd(cc + kWorkSlot + i, g_work[wave][i]);
 #ifdef RT_KSTATS
         for (int i = 0; i < 8; ++i) atomicAdd(cc + 3 + i, g_kst[wave][i]);

@@ -344,6 +344,7 @@ struct GpuRenderer : Renderer {
                 total.samples += st.samples;
                 total.ray_segments += st.ray_segments;
                 total.lane_slots += st.lane_slots;
+                total.direct_sky_samples += st.direct_sky_samples;
                 total.bounce_iters += st.bounce_iters;
             }
         if (range_err) throw Panic("assertion failed: a pixel channel exceeded 2.0 (color.rs:55-57)");

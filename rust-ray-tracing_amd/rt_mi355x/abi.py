@@ -69,7 +69,32 @@ class RtStats(ctypes.Structure):
         ("exact_tests", u64),
         ("cone_tests", u64),
         ("camera_exact_tests", u64),
+        ("direct_sky_samples", u64),
+        ("kernel_id", u32),
+        ("kernel_wg_per_cu", u32),
     ]
+
+
+def kernel_info(kernel_id):
+    """rt_stats.kernel_id decoded (include/rt_mi355x.h RT_KERNEL_*): the trace_paths instantiation that ran."""
+    if kernel_id == 0:
+        return None
+    return {"T": "double" if kernel_id & 1 else "float", "W": (kernel_id >> 1) & 7, "root2": bool((kernel_id >> 4) & 1),
+            "mode": (kernel_id >> 5) & 3, "camq": bool((kernel_id >> 7) & 1), "mega": bool((kernel_id >> 8) & 1)}
+
+
+def kernel_name(kernel_id):
+    """trace_paths<T,W,ROOT2,MODE,CAMQ,MEGA> as rocprofv3 lists it, e.g. trace_paths<float,6,false,0,true,false>."""
+    k = kernel_info(kernel_id)
+    if k is None:
+        return None
+    b = lambda v: "true" if v else "false"
+    return f"trace_paths<{k['T']},{k['W']},{b(k['root2'])},{k['mode']},{b(k['camq'])},{b(k['mega'])}>"
+
+
+def lane_utilisation(st):
+    """Enabled rays / SIMD lanes issued; pixels finished at claim time hold no lane (rt_stats)."""
+    return (st.ray_segments - st.direct_sky_samples) / max(1, st.lane_slots)
 
 
 # Executed FLOP per lane of one wave-level test (include/rt_mi355x.h, DESIGN.md §5); x 64 lanes.

@@ -46,6 +46,12 @@ import math
 import numpy as np
 
 F32 = np.float32
+# The fp32 reading relies on NumPy 2's scalar promotion (NEP 50): float32 combined with a Python float
+# stays float32.  Under NumPy 1.x expressions such as 2.0*ux-1.0 or t*4.0 would silently turn float64,
+# and the committed fp32 goldens would disagree in ways that look like kernel bugs.
+if type(F32(1) * 1.0) is not F32:
+    raise ImportError(f"tests/independent_v2.py needs NumPy >= 2 scalar promotion (NEP 50); numpy {np.__version__} "
+                      "promotes float32 * float to float64")
 
 # ---------------------------------------------------------------- exact fused multiply-add (f64)
 _TWO53 = float(1 << 53)

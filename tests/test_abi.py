@@ -61,6 +61,12 @@ int main(void) {
   P(rt_scene, center) P(rt_scene, radius) P(rt_scene, material) P(rt_scene, materials)
   P(rt_camera, center) P(rt_camera, ulc) P(rt_camera, dv)
   P(rt_stats, kernel_ms) P(rt_stats, ray_segments) P(rt_stats, bounce_iters)
+  P(rt_stats, camera_exact_tests) P(rt_stats, direct_sky_samples) P(rt_stats, kernel_id) P(rt_stats, kernel_wg_per_cu)
+  /* rt_stats.kernel_id's fields: trace_paths<double,4,true,3,true,true> and <float,6,false,0,true,false> */
+  printf("id_a %u,%u,%u,%u,%u,%u\n", RT_KERNEL_F64(0x81F9u), RT_KERNEL_WAVES(0x81F9u), RT_KERNEL_ROOT2(0x81F9u),
+         RT_KERNEL_MODE(0x81F9u), RT_KERNEL_CAMQ(0x81F9u), RT_KERNEL_MEGA(0x81F9u));
+  printf("id_b %u,%u,%u,%u,%u,%u\n", RT_KERNEL_F64(0x808Cu), RT_KERNEL_WAVES(0x808Cu), RT_KERNEL_ROOT2(0x808Cu),
+         RT_KERNEL_MODE(0x808Cu), RT_KERNEL_CAMQ(0x808Cu), RT_KERNEL_MEGA(0x808Cu));
   return 0;
 }
 """
@@ -80,6 +86,14 @@ def test_struct_layouts_match_c(tmp_path):
     }
     for k, v in py.items():
         assert int(got[k]) == v, k
+    # the header's RT_KERNEL_* macros and abi.kernel_info decode kernel_id alike
+    for tag, kid in (("id_a", 0x81F9), ("id_b", 0x808C)):
+        k = abi.kernel_info(kid)
+        want = [int(k["T"] == "double"), k["W"], int(k["root2"]), k["mode"], int(k["camq"]), int(k["mega"])]
+        assert [int(x) for x in got.pop(tag).split(",")] == want, tag
+    assert abi.kernel_name(0x808C) == "trace_paths<float,6,false,0,true,false>"
+    assert abi.kernel_name(0x81F9) == "trace_paths<double,4,true,3,true,true>"
+    assert abi.kernel_info(0) is None
     for key, val in got.items():
         if "." in key:
             st, field = key.split(".")

@@ -92,9 +92,10 @@ def test_empty_scene(renderer):
 @pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
 @pytest.mark.parametrize("spp", [1, 6, 100, 512])
 def test_sky_pixels(renderer, spp, flags, depth):
-    """Every sample escapes at bounce 0, so every pixel takes finish_pixel's sky path (no position map,
-    no replay, no colour reads; the slot's bounce flag stays clear): partial chunks (1, 6), quirk Q3's
-    other buffer (100), config C's spp (512), both precisions."""
+    """Every sample escapes at bounce 0.  With this pinhole camera every pixel's camera candidate list is
+    empty, so trace_paths finishes it when it claims it (finish_sky_direct: no slot, no lanes, no
+    records); test_sky_pixels_defocus takes finish_pixel's sky path instead.  Partial chunks (1, 6),
+    quirk Q3's other buffer (100), config C's spp (512), both precisions."""
     flat = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((0.5, 0.5, 0.5))])
     assert_parity(renderer, flat, cam_for(16, 9), depth, spp, flags)
 
@@ -691,3 +692,136 @@ def test_pixel_lists_overflow_and_straddle(renderer, flags):
     mats = [rt.Lambertian((0.7, 0.6, 0.5)), rt.Metal((0.9, 0.9, 0.9), 0.1), rt.Dielectric(1.5, False)]
     flat = rt.FlatScene(np.array(c), np.array(r), rng.integers(0, 3, len(r)).astype(np.uint32), mats)
     assert_parity(renderer, flat, cam_for(31, 17), 50, 100, flags)
+
+
+# ---- the benched kernels at their production launch shapes, against the independent restatement ----
+PRODUCTION_SHAPES = [
+    # (golden case, shards, kernel the launch must run)
+    ("C_f32", 1, "trace_paths<float,6,false,0,true,false>"),    # bench.py's headline line
+    ("C_f64", 1, "trace_paths<double,4,false,0,true,false>"),   # bench.py's f64 leg
+    ("D_f32", 8, "trace_paths<float,6,false,0,true,false>"),    # one rank of the 8-GPU D run
+    ("E_f32", 8, "trace_paths<float,6,false,0,true,true>"),     # the mega kernel, one rank of E
+    ("E_f64", 8, "trace_paths<double,4,false,0,true,true>"),
+]
+
+
+@pytest.mark.parametrize("name,shards,kernel", PRODUCTION_SHAPES)
+def test_production_shapes_vs_independent(renderer, name, shards, kernel, monkeypatch):
+    """The kernels bench.py times, launched as bench.py launches them (C: the whole 1920x1080 frame; D and
+    E: the 8 row shards of a 3840x2160 frame, bench.py --gpus 8), each compared bit for bit with the
+    INDEPENDENT restatement's pixels that fall inside it (tests/golden/independent_baseline.npz: linear
+    value and RGB8 bytes; its per-pixel ray segments are pinned by test_independent_baseline_golden).
+    rt_stats.kernel_id says which trace_paths instantiation ran, so this pins the timed kernel itself,
+    not the small-launch W5 build that 1x1 tiles take; kernel_wg_per_cu says it ran at its occupancy."""
+    monkeypatch.delenv("RT_WAVES", raising=False)
+    monkeypatch.delenv("RT_FILTER_OFF", raising=False)
+    z, meta = _baseline_cases()
+    m = meta[name]
+    W, H = m["W"], m["H"]
+    flat = rt.scenes.config_scene(m["config"]).flatten()
+    cam = rt.camera_new_py(W, H, **m["camera"])
+    flags = abi.RT_FLAG_F32 if m["precision"] == "f32" else 0
+    pix = z[f"{name}_pix"].astype(np.int64)
+    got_lin = np.full((len(pix), 3), np.nan)
+    got_rgb = np.zeros((len(pix), 3), np.uint8)
+    for r in range(shards):
+        inside = np.nonzero((pix // W) % shards == r)[0]
+        if inside.size == 0:
+            continue
+        tile = rt.parallel.shard_range(W, H, shards, r) if shards > 1 else None
+        rgb, lin, st, rc = gpu(renderer, flat, cam, m["depth"], m["spp"], m["seed"], flags, tile=tile)
+        assert rc == 0, (name, r)
+        assert abi.kernel_name(st.kernel_id) == kernel, (name, r, abi.kernel_name(st.kernel_id))
+        assert st.kernel_wg_per_cu == abi.kernel_info(st.kernel_id)["W"], (name, r, st.kernel_wg_per_cu)
+        # compact shard index of frame pixel q: (row // shards) * W + col
+        q = pix[inside]
+        at = (q // W // shards) * W + q % W
+        got_lin[inside] = lin[at]
+        got_rgb[inside] = rgb[at]
+    np.testing.assert_array_equal(got_lin, z[f"{name}_lin"], err_msg=name)
+    np.testing.assert_array_equal(got_rgb, z[f"{name}_rgb"], err_msg=name)
+
+
+@pytest.mark.parametrize("w,h,spp,flags,waves", [
+    (1920, 1080, 512, abi.RT_FLAG_F32, 6),   # big fp32 launch: W6
+    (64, 36, 512, abi.RT_FLAG_F32, 5),       # small fp32 launch: W5
+    (1920, 1080, 16, 0, 4),                  # fp64: W4
+    (64, 36, 16, abi.RT_FLAG_F32 | abi.RT_FLAG_MODE_SCALAR, 6),   # semantics modes: kWavesModes
+    (64, 36, 16, abi.RT_FLAG_MODE_VECTORIZED3, 4),
+    (64, 36, 16, abi.RT_FLAG_F32 | abi.RT_FLAG_ROOT2, 6),
+])
+def test_kernel_runs_at_its_occupancy(renderer, scene_100, w, h, spp, flags, waves, monkeypatch):
+    """rt_stats.kernel_id / kernel_wg_per_cu: every default kernel pick is resident at the waves per SIMD
+    it was built for (LDS and registers within the budget), 4-wave workgroups so W of them per CU."""
+    monkeypatch.delenv("RT_WAVES", raising=False)
+    _, _, st, rc = gpu(renderer, scene_100, cam_for(w, h), 8, spp, flags=flags)
+    assert rc == 0
+    k = abi.kernel_info(st.kernel_id)
+    assert k["W"] == waves and k["T"] == ("float" if flags & abi.RT_FLAG_F32 else "double"), abi.kernel_name(st.kernel_id)
+    assert st.kernel_wg_per_cu == waves
+    assert k["camq"]   # pinhole camera, depth >= 1
+
+
+@pytest.mark.parametrize("flags", [abi.RT_FLAG_F32, 0])
+def test_every_wave_override_resident(renderer, scene_100, flags, monkeypatch):
+    """RT_WAVES 4..8 (clamped to what each precision's LDS allows: fp32 6, fp64 5), on the pinhole and
+    the defocus paths and the mega kernels: each launch's kernel is resident at no less than its own W."""
+    flat_e = rt.scenes.config_scene("E").flatten()
+    for wv in ("4", "5", "6", "7", "8"):
+        monkeypatch.setenv("RT_WAVES", wv)
+        for flat, cam in ((scene_100, cam_for(32, 18)), (scene_100, _cam(32, 18, defocus_angle=2.0)), (flat_e, cam_for(8, 6))):
+            _, _, st, rc = gpu(renderer, flat, cam, 8, 8, flags=flags)
+            assert rc == 0
+            k = abi.kernel_info(st.kernel_id)
+            # at least its own W (a W4 fp32 build needs few enough registers for 5)
+            assert st.kernel_wg_per_cu >= k["W"] and k["W"] <= (6 if flags else 5), (wv, abi.kernel_name(st.kernel_id))
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+@pytest.mark.parametrize("spp", [1, 6, 100, 512])
+def test_sky_pixels_defocus(renderer, spp, flags):
+    """Every sample escapes at bounce 0 through a defocus camera (no camera batches, no candidate lists):
+    each pixel takes finish_pixel's sky path (K = 1 known from the slot's bounce flag: no position map,
+    no replay, no colour reads), with several pixels per wave."""
+    flat = rt.FlatScene(np.zeros((0, 3)), np.zeros(0), np.zeros(0, np.uint32), [rt.Lambertian((0.5, 0.5, 0.5))])
+    _, _, st, _ = gpu(renderer, flat, _cam(16, 9, defocus_angle=2.0), 50, spp, flags=flags)
+    assert not abi.kernel_info(st.kernel_id)["camq"] and st.direct_sky_samples == 0
+    assert_parity(renderer, flat, _cam(16, 9, defocus_angle=2.0), 50, spp, flags)
+
+
+@pytest.mark.parametrize("flags", [0, abi.RT_FLAG_F32])
+def test_mega_scene_whole_image(renderer, flags):
+    """Config E's 10 000-sphere scene through the mega kernels on a whole 64x36 image: sky rows finished
+    at claim time (finish_sky_direct saves and restores the lane's parked sample/slot word around it
+    while other lanes of the wave hold live rays) mixed with hit pixels, several pixels per wave, every
+    pixel against the oracle."""
+    flat = rt.scenes.config_scene("E").flatten()
+    lin, st = assert_parity(renderer, flat, cam_for(64, 36), 50, 16, flags)
+    assert abi.kernel_info(st.kernel_id)["mega"]
+    assert 0 < st.direct_sky_samples < 64 * 36 * 16   # both kinds of pixel
+
+
+def test_camera_table_cache_keys(renderer, scene_100, monkeypatch):
+    """The per-launch camera tables are cached per precision under (scene, camera centre bits, scalar
+    mode, RT_FILTER_OFF).  One context, one scene, every key left and returned to: centre A, B, A;
+    scalar then live path; fp32 and fp64 interleaved; RT_FILTER_OFF on and off.  Each render equals the
+    oracle's, so no stale table is ever reused."""
+    monkeypatch.delenv("RT_FILTER_OFF", raising=False)
+    cam_a = cam_for(32, 18)
+    cam_b = _cam(32, 18, center=(14.0, 3.0, 17.0))
+    seq = [(cam_a, 0, 0), (cam_b, 0, 0), (cam_a, 0, 0),
+           (cam_a, abi.RT_FLAG_F32, 0), (cam_b, abi.RT_FLAG_F32, 0), (cam_a, 0, 0),
+           (cam_a, abi.RT_FLAG_MODE_SCALAR, 0), (cam_a, 0, 0), (cam_a, abi.RT_FLAG_MODE_SCALAR | abi.RT_FLAG_F32, 0),
+           (cam_a, abi.RT_FLAG_F32, 0), (cam_a, abi.RT_FLAG_F32, 1), (cam_a, abi.RT_FLAG_F32, 0), (cam_b, 0, 1),
+           (cam_a, 0, 0)]
+    renderer.set_scene(scene_100)
+    for i, (cam, flags, off) in enumerate(seq):
+        if off:
+            monkeypatch.setenv("RT_FILTER_OFF", "1")
+        else:
+            monkeypatch.delenv("RT_FILTER_OFF", raising=False)
+        rgb, lin, st, rc = gpu(renderer, scene_100, cam, 50, 8, flags=flags)
+        prec = "f32" if flags & abi.RT_FLAG_F32 else "f64"
+        _, lin_o, segs_o, _ = oracle_render(scene_100, cam, 50, 8, SEED, flags & ~abi.RT_FLAG_F32, precision=prec)
+        np.testing.assert_array_equal(lin, lin_o, err_msg=f"step {i}")
+        assert st.ray_segments == segs_o, i

@@ -96,8 +96,8 @@ def test_baseline_sizes_oracle_spots(renderer, config, flags, stride, n_spot):
 
 # ---------------------------------------------------------------- occupancy builds, bit for bit
 @pytest.mark.parametrize("config,flags,waves", [
-    ("C", abi.RT_FLAG_F32, ("4", "5", "6", "7")),   # the whole benched frame (>= 32768 samples per wave)
-    ("B", 0, ("4", "5")),
+    ("C", abi.RT_FLAG_F32, ("4", "5", "6", "7")),   # the whole benched frame; 7 is clamped to 6
+    ("B", 0, ("4", "5", "6")),                      # fp64: 6 is clamped to 5
 ])
 def test_wave_builds_bit_identical(renderer, monkeypatch, config, flags, waves):
     """RT_WAVES selects the register-allocation target (waves per SIMD) at every launch; every

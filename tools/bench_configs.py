@@ -36,7 +36,7 @@ def run(config, precision, stride):
             "roofline_frac": round(sum(f / (pk * 1e12) for f, pk in zip(abi.executed_flop(st, precision), (157.3, 78.6)))
                                    / (st.kernel_ms / 1e3), 4),
             "segments_per_sample": round(st.ray_segments / samples, 4),
-            "lane_utilisation": round(st.ray_segments / max(1, st.lane_slots), 4), "wall_s": round(wall, 2)}
+            "lane_utilisation": round(rt.abi.lane_utilisation(st), 4), "wall_s": round(wall, 2)}
 
 
 if __name__ == "__main__":
