@@ -152,6 +152,76 @@ __device__ __forceinline__ T reduce_positions(uint32_t P, uint32_t* hist, T (*st
     return lane < 12u ? accl[lane] : T(0.0);
 }
 
+
+// The live path's final reduction (ray_tracing.rs:488-504) over whole batches of 64 positions with a u16
+// position map (LDS or the wave's scratch): the same values and the same order of adds as
+// reduce_positions with finish_pixel's generic value lambda (the partial last batch, spp % 64, goes through
+// that lambda), specialised: no bounds test in whole batches, a three-op map decode, a branch-free record
+// load for positions without an entry (clamped to a valid record, value 0), the y load independent of the
+// map, the next batch's map entry loaded before this batch's records, and the 12 running sums in a VGPR.
+template <typename T, typename G>
+__device__ __forceinline__ T reduce_live16(const PScratch<T>& sc, uint32_t s, uint32_t spp, uint32_t P, const uint16_t* lmap,
+                                           bool lm, uint32_t* hist, T (*stage)[64], G&& generic) {
+    const uint32_t lane = threadIdx.x & 63u;
+    T* accl = (T*)hist;
+    T racc = T(0.0);
+    if (lane < 12u) accl[lane] = T(0.0);
+    const uint32_t nfull = spp & ~63u;
+    const uint16_t* gmap = (const uint16_t*)sc.base;
+    const uint32_t si = 16u * (lane & 3u) + (lane >> 2);
+    uint32_t m16n = nfull ? (lm ? (uint32_t)lmap[lane] : (uint32_t)gmap[lane]) : 0xFFFFu;
+    for (uint32_t qb = 0; qb < nfull; qb += 64u) {
+        const uint32_t qq = qb + lane;
+        const T y = sc.y(s, qq);
+        const uint32_t m16 = m16n;
+        if (qb + 64u < nfull) m16n = lm ? (uint32_t)lmap[qq + 64u] : (uint32_t)gmap[qq + 64u];
+        const bool has = m16 != 0xFFFFu, wh = m16 >= 0x8000u;
+        const uint32_t smp = min(m16 & 0x7FFFu, spp - 1u);   // a clamped (unused) record without an entry
+        const C3<T> cm = sc.c(s, smp);
+        const V3<T> sk = sky(y);
+        const T vr = has ? (wh ? sk.x : cm.x * sk.x) : T(0.0);   // (white x sky) == sky, bit for bit
+        const T vg = has ? (wh ? sk.y : cm.y * sk.y) : T(0.0);
+        const T vb = has ? (wh ? sk.z : cm.z * sk.z) : T(0.0);
+        stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 12u) {
+            const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
+            T a = racc;
+#pragma unroll
+            for (uint32_t u0 = 0; u0 < 16u; u0 += 4u) {
+                T v[4];
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; ++u) v[u] = sv[u0 + u];
+#pragma unroll
+                for (uint32_t u = 0; u < 4u; ++u) a = a + v[u];
+            }
+            racc = a;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < 12u) accl[lane] = racc;
+    // the partial last batch (and positions past spp): the generic path, continuing the same sums
+    for (uint32_t qb = nfull; qb < P; qb += 64u) {
+        const uint32_t qq = qb + lane;
+        T vr = T(0.0), vg = T(0.0), vb = T(0.0);
+        if (qq < P) generic(qq, vr, vg, vb);
+        stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane < 12u) {
+            const uint32_t nu = min(16u, (P - qb) / 4u);
+            const T* sv = &stage[lane >> 2][16u * (lane & 3u)];
+            T a = accl[lane];
+            for (uint32_t u = 0; u < nu; ++u) a = a + sv[u];
+            accl[lane] = a;
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return lane < 12u ? accl[lane] : T(0.0);
+}
+
 // The pixel's value: PackedColor::sum of the 4 lanes' sums (or the scalar mode's average), / spp
 // (renderer.rs:161), Color::to_u8_array's assert and bytes (color.rs:54-64).
 template <typename T, int MODE>
@@ -298,25 +368,38 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const uint32_t ec = ret ? e : K;
                 const unsigned long long inm = __ballot(in);
                 // eq, gt: the lanes equal to / greater than this lane's ec; eqk: the lanes whose ec equals
-                // this lane's index k (lane k's count of e == k).  A plane no lane sets changes neither eq
-                // nor gt, and clears eqk in the lanes k with that bit (zb)
-                unsigned long long eq = inm, gt = 0ull, eqk = inm;
-                uint32_t zb = 0;
+                // this lane's index k (lane k's count of e == k).  The masks are kept as 32-bit halves, B and Bk
+                // all-ones or zero per lane (v_bfe_i32), each update one v_bitop3 / v_and_or per half (truth
+                // table index S0 << 2 | S1 << 1 | S2): 11 VALU per plane, where the 64-bit form took ~22 (the
+                // compiler built the lane masks with cndmasks).  Every plane is applied, without a branch (a
+                // skipped plane cost loop-carried copies): a plane no lane sets leaves eq and gt unchanged in the
+                // lanes that use them and clears eqk in the lanes k with that bit.  Round 5, same-box with the
+                // reduction below: C fp32 +1.9 %, fp64 +2.4 %, E +1.3 % (profiles/r05/finish_ab.txt).
+                uint32_t eql = (uint32_t)inm, eqh = (uint32_t)(inm >> 32), gtl = 0u, gth = 0u;
+                uint32_t eqkl = eql, eqkh = eqh;
                 for (uint32_t bb = nb; bb-- > 0u;) {
-                    const unsigned long long P = __ballot(in && ((ec >> bb) & 1u));
-                    if (P == 0ull) { zb |= 1u << bb; continue; }
-                    const unsigned long long B = ((ec >> bb) & 1u) ? ~0ull : 0ull;     // this lane's bit
-                    const unsigned long long Bk = ((lane >> bb) & 1u) ? ~0ull : 0ull;  // bit of k = lane
-                    gt |= eq & P & ~B;     // equal so far, 1 where this lane has 0: greater
-                    eq &= ~(P ^ B);        // still equal
-                    eqk &= ~(P ^ Bk);
+                    const uint32_t B = (uint32_t)__builtin_amdgcn_sbfe((int)ec, bb, 1u);     // this lane's bit
+                    const unsigned long long P = __ballot(B != 0u) & inm;
+                    const uint32_t Pl = (uint32_t)P, Ph = (uint32_t)(P >> 32);
+                    const uint32_t Bk = (uint32_t)__builtin_amdgcn_sbfe((int)lane, bb, 1u);  // bit of k = lane
+                    // gt |= eq & P & ~B (equal so far, 1 where this lane has 0: greater)
+                    gtl = ((eql & ~B) & Pl) | gtl;
+                    gth = ((eqh & ~B) & Ph) | gth;
+                    // eq &= ~(P ^ B) (still equal), eqk &= ~(P ^ Bk): table 0x90
+                    eql = __builtin_amdgcn_bitop3_b32(eql, Pl, B, 0x90);
+                    eqh = __builtin_amdgcn_bitop3_b32(eqh, Ph, B, 0x90);
+                    eqkl = __builtin_amdgcn_bitop3_b32(eqkl, Pl, Bk, 0x90);
+                    eqkh = __builtin_amdgcn_bitop3_b32(eqkh, Ph, Bk, 0x90);
                 }
+                const unsigned long long eq = ((unsigned long long)eqh << 32) | eql;
+                const unsigned long long gt = ((unsigned long long)gth << 32) | gtl;
+                const unsigned long long eqk = ((unsigned long long)eqkh << 32) | eqkl;
                 const uint32_t ek = ret ? e : 0u;
                 // the earlier chunks' counts at this lane's bounce
                 const uint32_t cg = (uint32_t)__shfl((int)cge, (int)ek), cq = (uint32_t)__shfl((int)ceq, (int)ek);
                 const uint32_t nn = (uint32_t)__shfl((int)nn_l, (int)ek);
                 // lane k < K: #{e == k} in this chunk (lanes k >= 2^nb or > K are never read)
-                const uint32_t h = (lane & zb) != 0u ? 0u : (uint32_t)__popcll(eqk);
+                const uint32_t h = (uint32_t)__popcll(eqk);
                 // lane k <= K: #{in && e >= k} = #{in} - #{e < k}
                 cge += (uint32_t)__popcll(inm) - (wave_scan_dpp(h) - h);
                 ceq += h;
@@ -475,7 +558,7 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     } else {
         const V3<T> s0 = sky(T(0.0));
         const bool white0 = depth == 0u && q.s_sel == 0u;
-        acc = reduce_positions<T>(P, hist, stage, [&](uint32_t qq, T& vr, T& vg, T& vb) {
+        auto vals = [&](uint32_t qq, T& vr, T& vg, T& vb) {
             if (MODE == kModeV3) {
                 // the sample at slot qq: its own value; a missing lane (white, hit_sky at bounce 0
                 // with a zero direction) adds sky(0), or white when no bounce ran (:611-619)
@@ -512,7 +595,9 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
                 const C3<T> cm = sc.c(s, qq);
                 vr = cm.x; vg = cm.y; vb = cm.z;
             }
-        });
+        };
+        if (MODE == kModeV2 && !sky_only && !(sc.wide & 2u)) acc = reduce_live16<T>(sc, s, spp, P, lmap, lm, hist, stage, vals);
+        else acc = reduce_positions<T>(P, hist, stage, vals);
     }
     write_pixel<T, MODE>(acc, item);
     return K;
