@@ -360,7 +360,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         l2 = pk_len2(vec);
     }
     const T len = (SCALAR && !cam) ? rad : sqrt(l2);
-    const V3<T> u = mk(vec.x / len, vec.y / len, vec.z / len);
+    const V3<T> u = dvs(vec, len);
     if (cam) {
         o = base;
         d = u;
@@ -386,7 +386,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         const T ratio = front ? m.inv_ior : m.ior;
         const V3<T> nn = m.hollow ? neg(nrm) : nrm;
         const T ct = fmin(dot(neg(d), nn), T(1.0));
-        const T st = sqrt(T(1.0) - ct * ct);
+        const T st = sqrt_nd(T(1.0) - ct * ct);   // ct <= 1: 0, >= 2^-24 or negative
         bool refl = ratio * st > T(1.0);
         if (!refl) {   // Dielectric::reflectance (materials.rs:121-124), powi(5) = x*((x*x)*(x*x))
             const T r0 = front ? m.r0_front : m.r0_back;

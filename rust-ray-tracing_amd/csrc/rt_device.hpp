@@ -20,6 +20,38 @@ template <typename T> __device__ __forceinline__ V3<T> add(V3<T> a, V3<T> b) { r
 template <typename T> __device__ __forceinline__ V3<T> sub(V3<T> a, V3<T> b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 template <typename T> __device__ __forceinline__ V3<T> mul(V3<T> a, T s) { return mk(a.x * s, a.y * s, a.z * s); }
 template <typename T> __device__ __forceinline__ V3<T> dvs(V3<T> a, T s) { return mk(a.x / s, a.y / s, a.z / s); }
+// a / |a| for fp32 (unit(), next_ray's normal): the compiler's correctly rounded division is
+// div_scale x2, rcp, 6 FMAs, div_fmas, div_fixup per component; when v_div_scale would scale nothing and
+// div_fixup has no special case to fix (every lane: 2^-20 <= len <= 2^20 and every |component| >= 2^-100,
+// which bounds |a_i / len| by ~1 since |a_i| <= len), the same sequence without them gives the same bits,
+// with the denominator's refined reciprocal shared by the three components.  Otherwise the full division.
+template <> __device__ __forceinline__ V3<float> dvs(V3<float> a, float s) {
+    const float mn = fminf(fminf(fabsf(a.x), fabsf(a.y)), fabsf(a.z));
+    const bool ok = s >= 0x1.0p-20f && s <= 0x1.0p20f && mn >= 0x1.0p-100f;
+    if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
+        const float r0 = __builtin_amdgcn_rcpf(s);
+        const float r1 = __builtin_fmaf(__builtin_fmaf(-s, r0, 1.0f), r0, r0);
+        auto q = [&](float x) {
+            const float m = x * r1;
+            const float f3 = __builtin_fmaf(__builtin_fmaf(-s, m, x), r1, m);
+            return __builtin_fmaf(__builtin_fmaf(-s, f3, x), r1, f3);
+        };
+        return mk(q(a.x), q(a.y), q(a.z));
+    }
+    return mk(a.x / s, a.y / s, a.z / s);
+}
+// sqrt, correctly rounded, of an argument known to be +-0, >= 2^-96, +inf, negative or NaN (never a tiny
+// positive one): v_sqrt_f32 (within 1 ulp) and the compiler's own correction by the residuals of the two
+// neighbours, without its scaling for arguments below 2^-96 and its special-value select (both no-ops
+// here: 0, +inf and NaN come through the correction unchanged).  fp64: the library sqrt.
+__device__ __forceinline__ float sqrt_nd(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sdn = __int_as_float(__float_as_int(s) - 1), sup = __int_as_float(__float_as_int(s) + 1);
+    float r = __builtin_fmaf(-sdn, s, x) <= 0.0f ? sdn : s;
+    r = __builtin_fmaf(-sup, s, x) > 0.0f ? sup : r;
+    return r;
+}
+__device__ __forceinline__ double sqrt_nd(double x) { return sqrt(x); }
 template <typename T> __device__ __forceinline__ V3<T> neg(V3<T> a) { return mk(-a.x, -a.y, -a.z); }
 template <typename T> __device__ __forceinline__ T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 template <typename T> __device__ __forceinline__ T len2(V3<T> a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
@@ -39,7 +71,7 @@ template <typename T> __device__ __forceinline__ V3<T> reflect(V3<T> v, V3<T> n)
 template <typename T> __device__ __forceinline__ V3<T> refract(V3<T> v, V3<T> n, T ratio) {
     T ct = fmin(dot(neg(v), n), T(1.0));
     V3<T> rperp = mul(add(v, mul(n, ct)), ratio);
-    V3<T> rpar = mul(n, -(sqrt(fabs(T(1.0) - len2(rperp)))));
+    V3<T> rpar = mul(n, -(sqrt_nd(fabs(T(1.0) - len2(rperp)))));   // |1 - x| is 0 or >= 2^-24
     return add(rperp, rpar);
 }
 
@@ -118,7 +150,7 @@ template <typename T> __device__ __forceinline__ void sincos2pi(T u, T& so, T& c
 // Uniform direction on S^2: the distribution of Vec3::random_unit_vector (geometry.rs:139-152).
 template <typename T> __device__ __forceinline__ V3<T> unit_vec(T u1, T u2) {
     const T z = T(1.0) - T(2.0) * u1;
-    const T r = sqrt(T(1.0) - z * z);
+    const T r = sqrt_nd(T(1.0) - z * z);   // z = 1 - 2 u1: 1 - z^2 is 0 or >= 2^-24
     T s, c;
     sincos2pi(u2, s, c);
     return mk(r * c, r * s, z);
