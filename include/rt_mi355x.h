@@ -33,6 +33,11 @@ extern "C" {
                                 Color::to_u8_array (color.rs:55-57); the image is still written */
 #define RT_ERR_UNSUPPORTED 4 /* configuration this build cannot run (e.g. spp > 2^20) */
 
+/* Largest max_bounces an RT_FLAG_F32 render accepts (RT_ERR_UNSUPPORTED above): fp32 draws Philox2x32-10
+ * with the counter (pixel, sample | code << 20), code 257 + bounce for the scatter, which must stay below
+ * 2^12.  fp64 (Philox4x32-10, the bounce in its own counter word) has no such limit. */
+#define RT_MAX_BOUNCES_F32 3839u
+
 /* ---- materials (src/materials.rs:41-155) ---- */
 #define RT_LAMBERTIAN 0u
 #define RT_METAL 1u

@@ -34,6 +34,21 @@ void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t
     out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
 }
 
+/* Philox2x32-10 (Random123 philox2x32 with R = 10): multiplier 0xD256D193, Weyl key bump 0x9E3779B9;
+ * round: hi:lo = M * c0, (c0, c1) <- (hi ^ key ^ c1, lo).  The fp32 build's draws (oracle_impl.h SFX(draw),
+ * rt_device.hpp rng<float>). */
+void oracle_philox2x32_10(const uint32_t ctr[2], uint32_t key, uint32_t out[2]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], k = key;
+    for (int i = 0; i < 10; ++i) {
+        uint64_t p = (uint64_t)0xD256D193u * c0;
+        uint32_t n0 = (uint32_t)(p >> 32) ^ k ^ c1;
+        c1 = (uint32_t)p;
+        c0 = n0;
+        k += 0x9E3779B9u;
+    }
+    out[0] = c0; out[1] = c1;
+}
+
 /* ---------------- f64 instantiation (the reference's arithmetic) ---------------- */
 #define REAL double
 #define SFX(x) x##_f64

@@ -73,7 +73,9 @@ typedef struct or_camera {
  * gamma), either may be NULL.  *segments (may be NULL) receives the number of
  * enabled rays traced (sum over bounces of enabled lanes).
  * Returns 0, or 3 if some channel exceeded 2.0 (the reference panics there,
- * color.rs:55-57), or 1 on bad arguments (including both mode bits set). */
+ * color.rs:55-57), or 1 on bad arguments (including both mode bits set), or 4 when the
+ * RNG counter cannot hold the configuration (spp > 2^20; f32: max_bounces > 3839, the
+ * C ABI's RT_ERR_UNSUPPORTED). */
 int oracle_render_f64(const or_scene* sc, const or_camera* cam, uint32_t max_bounces,
                       uint32_t spp, uint64_t seed, uint32_t flags,
                       const uint32_t* pixels, uint32_t n_pixels,
@@ -90,6 +92,8 @@ int oracle_camera_new(or_camera* out, uint32_t w, uint32_t h, double focal_lengt
 
 /* Philox4x32-10 block (for KATs). */
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* Philox2x32-10 block: the fp32 build's draws (for KATs). */
+void oracle_philox2x32_10(const uint32_t ctr[2], uint32_t key, uint32_t out[2]);
 
 /* Primitive probes for known-answer tests. */
 void oracle_sincos2pi_f64(double u, double* s, double* c);

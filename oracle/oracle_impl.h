@@ -69,6 +69,23 @@ static inline REAL SFX(u01b)(const uint32_t* r) {  /* second independent uniform
 #endif
 }
 
+/* One draw block for (sample, pixel, k, stream) (the kernel's rng<T>, rt_device.hpp): stream 0 the camera
+ * jitter (k = 0), 1 disk try k, 2 the scatter at bounce k.  f64: Philox4x32-10, counter (sid, pix, k,
+ * stream), key (seed lo, seed hi).  f32 uses two 24-bit words only: Philox2x32-10, counter
+ * (pix, sid | code << 20) with code 0 / 1 + k / 257 + k, key seed lo ^ seed hi (r[2], r[3] unused). */
+static inline void SFX(draw)(uint32_t sid, uint32_t pix, uint32_t k, uint32_t stream, uint32_t k0, uint32_t k1,
+                             uint32_t r[4]) {
+#if ORACLE_IS_F64
+    const uint32_t ctr[4] = {sid, pix, k, stream}, key[2] = {k0, k1};
+    oracle_philox4x32_10(ctr, key, r);
+#else
+    const uint32_t code = stream == 0u ? 0u : (stream == 1u ? 1u + k : 257u + k);
+    const uint32_t ctr[2] = {pix, sid | (code << 20)};
+    oracle_philox2x32_10(ctr, k0 ^ k1, r);
+    r[2] = 0u; r[3] = 0u;
+#endif
+}
+
 /* sin(2*pi*u), cos(2*pi*u) for u in [0,1): exact quadrant/octant reduction in u-space, then
  * Taylor polynomials on [0, pi/4] evaluated by fma-Horner (bit-identical on CPU and GPU). */
 static inline void SFX(sincos2pi)(REAL u, REAL* so, REAL* co) {
@@ -150,8 +167,8 @@ typedef struct {
 /* Camera::get_ray, ray_tracing.rs:77-89 */
 static void SFX(get_ray)(const SFX(cam_r)* c, uint32_t col, uint32_t row, uint32_t pix, uint32_t s,
                          uint32_t k0, uint32_t k1, V3* o, V3* d) {
-    uint32_t ctr[4] = {s, pix, 0u, 0u}, key[2] = {k0, k1}, r[4];
-    oracle_philox4x32_10(ctr, key, r);
+    uint32_t r[4];
+    SFX(draw)(s, pix, 0u, 0u, k0, k1, r);
     REAL xo = SFX(u01)(r), yo = SFX(u01b)(r);
     REAL s1 = ((REAL)col + xo) / (REAL)c->W;
     REAL s2 = ((REAL)row + yo) / (REAL)c->H;
@@ -160,8 +177,7 @@ static void SFX(get_ray)(const SFX(cam_r)* c, uint32_t col, uint32_t row, uint32
     /* random_in_unit_disk: rejection on [-1,1]^2 (geometry.rs:154-168) */
     REAL dx = 0, dy = 0;
     for (uint32_t i = 0; i < 256u; ++i) {
-        uint32_t c2[4] = {s, pix, i, 1u};
-        oracle_philox4x32_10(c2, key, r);
+        SFX(draw)(s, pix, i, 1u, k0, k1, r);
         REAL x = (REAL)2.0 * SFX(u01)(r) - (REAL)1.0;
         REAL y = (REAL)2.0 * SFX(u01b)(r) - (REAL)1.0;
         if (x * x + y * y <= (REAL)1.0) { dx = x; dy = y; break; }
@@ -246,8 +262,8 @@ static inline void SFX(finalize)(const SFX(prays)* R, SFX(phit)* H) {
  * 128-147 (dielectric).  Writes the scattered ray; returns attenuation. */
 static inline void SFX(scatter)(const SFX(mat_r)* m, V3 d, V3 p, V3 n, int front, uint32_t pix, uint32_t sid,
                                 uint32_t k, uint32_t k0, uint32_t k1, V3* od, REAL att[3]) {
-    uint32_t ctr[4] = {sid, pix, k, 2u}, key[2] = {k0, k1}, r[4];
-    oracle_philox4x32_10(ctr, key, r);
+    uint32_t r[4];
+    SFX(draw)(sid, pix, k, 2u, k0, k1, r);
     (void)p;
     if (m->kind == 0u) {
         V3 sd = SFX(add)(SFX(unit_vec)(SFX(u01)(r), SFX(u01b)(r)), n);
@@ -728,6 +744,10 @@ int SFX(oracle_render)(const or_scene* sc, const or_camera* cam, uint32_t max_bo
                        const uint32_t* pixels, uint32_t n_pixels,
                        uint8_t* rgb_out, double* lin_out, uint64_t* segments, int n_threads) {
     if (!sc || !cam || spp == 0 || cam->image_width == 0 || cam->image_height == 0) return 1;
+    if (spp > (1u << 20)) return 4;                   /* SFX(draw)'s counters */
+#if !ORACLE_IS_F64
+    if (max_bounces > 3839u) return 4;                /* 257 + bounce < 2^12 (RT_MAX_BOUNCES_F32) */
+#endif
     {
         const uint32_t modes = flags & (OR_FLAG_MODE_VECTORIZED | OR_FLAG_MODE_SCALAR | OR_FLAG_MODE_VECTORIZED3);
         if (modes & (modes - 1u)) return 1;   /* at most one mode */

@@ -319,7 +319,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
                                          uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
     const U4 r = [&] {
         const auto& q0 = *cold_args<T>();
-        return philox(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
+        return rng<T>(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
     }();
     const auto& q = *cold_args_after<T>(r.a ^ r.b);
     const T ua = u01a(r, T(0)), ub = u01b(r, T(0));
@@ -343,7 +343,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
                 // the camera constants on every iteration, pinhole or not.
                 uint32_t k0 = q.k0, k1 = q.k1;
                 asm volatile("" : "+s"(k0), "+s"(k1));
-                const U4 qq = philox(sid, pix, i, 1u, k0, k1);
+                const U4 qq = rng<T>(sid, pix, i, 1u, k0, k1);
                 const T x = T(2.0) * u01a(qq, T(0)) - T(1.0);
                 const T y = T(2.0) * u01b(qq, T(0)) - T(1.0);
                 if (x * x + y * y <= T(1.0)) { dx = x; dy = y; break; }

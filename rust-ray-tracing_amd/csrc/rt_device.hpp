@@ -90,6 +90,32 @@ __device__ __forceinline__ U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint
     }
     return U4{c0, c1, c2, c3};
 }
+// Philox2x32-10 (Random123's philox2x32, R = 10): one 32x32->64 product and one three-way xor per round.
+__device__ __forceinline__ U4 philox2(uint32_t c0, uint32_t c1, uint32_t k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint64_t p = (uint64_t)0xD256D193u * c0;
+        c0 = __builtin_amdgcn_bitop3_b32((uint32_t)(p >> 32), c1, k, 0x96);
+        c1 = (uint32_t)p;
+        k += 0x9E3779B9u;
+    }
+    return U4{c0, c1, 0u, 0u};
+}
+// One draw block for (sample, pixel, k, stream): stream 0 the camera jitter (k = 0), 1 disk try k, 2 the
+// scatter at bounce k.  fp64 takes two 53-bit uniforms from Philox4x32-10, counter (sample, pixel, k,
+// stream), key (seed lo, seed hi).  fp32 needs only two 24-bit uniforms, so it draws Philox2x32-10 with
+// counter (pixel, sample | code << 20), code = 0 / 1 + k / 257 + k, key seed lo ^ seed hi: half the
+// multiplies (round 5, same-box C fp32 +1.9 %).  The host keeps the counter injective: spp <= 2^20 and,
+// in fp32, max_bounces <= RT_MAX_BOUNCES_F32 (257 + k < 2^12).
+template <typename T>
+__device__ __forceinline__ U4 rng(uint32_t sid, uint32_t pix, uint32_t k, uint32_t stream, uint32_t k0, uint32_t k1) {
+    if constexpr (sizeof(T) == 4) {
+        const uint32_t code = stream == 0u ? 0u : (stream == 1u ? 1u + k : 257u + k);
+        return philox2(pix, sid | (code << 20), k0 ^ k1);
+    } else {
+        return philox(sid, pix, k, stream, k0, k1);
+    }
+}
 // Uniform [0,1): f64 from 53 bits of (a,b) / (c,d); f32 from 24 bits of a / b.
 __device__ __forceinline__ double u01a(const U4& r, double) { return (double)((((uint64_t)r.a << 32) | r.b) >> 11) * 0x1.0p-53; }
 __device__ __forceinline__ double u01b(const U4& r, double) { return (double)((((uint64_t)r.c << 32) | r.d) >> 11) * 0x1.0p-53; }

@@ -255,7 +255,7 @@ __device__ __forceinline__ void finish_sky_direct(uint32_t item, uint32_t col, u
     const T acc = reduce_positions<T>(q.P, hist, stage, [&](uint32_t qq, T& vr, T& vg, T& vb) {
         if (qq >= spp) { vr = s0.x; vg = s0.y; vb = s0.z; return; }
         const auto& qc = *cold_args<T>();
-        const U4 r = philox(qq, pix, 0u, 0u, qc.k0, qc.k1);
+        const U4 r = rng<T>(qq, pix, 0u, 0u, qc.k0, qc.k1);
         const T s1 = div_dim((T)col + u01a(r, T(0)), qc.W, qc.rW);
         const T s2 = div_dim((T)row + u01b(r, T(0)), qc.H, qc.rH);
         const V3<T> vu = mk(qc.vu[0], qc.vu[1], qc.vu[2]), vv = mk(qc.vv[0], qc.vv[1], qc.vv[2]);

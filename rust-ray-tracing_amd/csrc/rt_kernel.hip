@@ -647,6 +647,8 @@ extern "C" int rt_render_async(rt_context* c, const rt_camera* cam, uint32_t max
             return fail(RT_ERR_INVALID, "rt_render_async: the RT_FLAG_MODE_* flags are exclusive");
     }
     if (spp > (1u << 20)) return fail(RT_ERR_UNSUPPORTED, "rt_render_async: spp > 2^20");
+    if ((flags & RT_FLAG_F32) && max_bounces > RT_MAX_BOUNCES_F32)   // rng<float>'s counter (rt_device.hpp)
+        return fail(RT_ERR_UNSUPPORTED, "rt_render_async: fp32 with max_bounces > RT_MAX_BOUNCES_F32 (3839)");
     if (cam->image_width == 0 || cam->image_height == 0) return fail(RT_ERR_INVALID, "rt_render_async: empty image");
     if ((uint64_t)cam->image_width * cam->image_height > 0xFFFFFFFFull) return fail(RT_ERR_UNSUPPORTED, "image too large");
     rt_tile_range rg = range ? *range : rt_tile_range{0, 1, cam->image_height, 0, cam->image_width};

@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
         if (v) {   // Camera::get_ray (ray_tracing.rs:77-89) with origin == centre
             const U4 r = [&] {
                 const auto& q0 = *cold_args<T>();
-                return philox(bsid, bpix, 0u, 0u, q0.k0, q0.k1);
+                return rng<T>(bsid, bpix, 0u, 0u, q0.k0, q0.k1);
             }();
             const auto& q = *cold_args_after<T>(r.a ^ r.b);
             const T s1 = div_dim((T)bcol + u01a(r, T(0)), q.W, q.rW);

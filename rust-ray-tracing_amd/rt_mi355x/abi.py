@@ -16,6 +16,7 @@ RT_ERR_INVALID = 1
 RT_ERR_HIP = 2
 RT_ERR_RANGE = 3
 RT_ERR_UNSUPPORTED = 4
+RT_MAX_BOUNCES_F32 = 3839   # include/rt_mi355x.h: fp32 renders refuse more (RNG counter width)
 
 RT_LAMBERTIAN = 0
 RT_METAL = 1

@@ -9,6 +9,8 @@ linear f64 + rgb8 + ray segments.
 
   python tests/golden/make_independent_golden.py     # rewrites tests/golden/independent_v2.npz
   python tests/golden/make_independent_golden.py baseline   # rewrites tests/golden/independent_baseline.npz
+  python tests/golden/make_independent_golden.py baseline C_f32 --out /tmp/c.npz   # one case (parallel runs),
+  python tests/golden/make_independent_golden.py baseline-merge /tmp/c.npz ...      # then merged in
 
 The baseline set (round 4) pins the BASELINE.json configs at their real sizes: strided pixels of
 configs B, C, D and E (full image, camera, sphere count, spp and depth), in f64 (the reference's
@@ -81,9 +83,16 @@ def baseline_pixels(W, H, n):
     return [(k * step) % (W * H) for k in range(n)]
 
 
-def main_baseline():
+def main_baseline(names=None, out=OUT_BASELINE):
+    """The baseline cases (all, or the named ones merged into the existing file; out: where to write)."""
     data, meta = {}, {}
+    if names is not None and os.path.exists(OUT_BASELINE):
+        old = np.load(OUT_BASELINE)
+        meta = json.loads(str(old["meta"]))
+        data = {k: old[k] for k in old.files if k != "meta"}
     for name, (cfg, n, prec) in BASELINE_CASES.items():
+        if names is not None and name not in names:
+            continue
         W, H, nsph, spp, depth = rt.scenes.CONFIGS[cfg]
         flat = rt.scenes.config_scene(cfg).flatten()
         p, cam = camera(W, H, {})
@@ -104,8 +113,10 @@ def main_baseline():
         meta[name] = {"config": cfg, "W": W, "H": H, "spheres": nsph, "depth": depth, "spp": spp, "precision": prec,
                       "camera": p, "seed": SEED, "pixels": len(px)}
     data["meta"] = np.array(json.dumps(meta))
-    np.savez_compressed(OUT_BASELINE, **data)
-    print("wrote", OUT_BASELINE)
+    if out != OUT_BASELINE:
+        data["computed"] = np.array(json.dumps(sorted(names)))
+    np.savez_compressed(out, **data)
+    print("wrote", out)
 
 
 def main():
@@ -129,5 +140,30 @@ def main():
 if __name__ == "__main__":
     if sys.argv[1:] == ["baseline"]:
         main_baseline()
+    elif sys.argv[1:2] == ["baseline"]:
+        # baseline CASE... [--out FILE]: recompute the named cases (e.g. after a change of the fp32 draws:
+        # B_f32 C_f32 D_f32 E_f32), keeping the others; one process per case, then merge the outputs with
+        # baseline-merge FILE...
+        args = sys.argv[2:]
+        out = OUT_BASELINE
+        if "--out" in args:
+            i = args.index("--out")
+            out = args[i + 1]
+            args = args[:i] + args[i + 2:]
+        main_baseline(set(args), out)
+    elif sys.argv[1:2] == ["baseline-merge"]:
+        # a part file holds the whole set with its own case recomputed: take only that case (named by the
+        # part file's "computed" entry) from it
+        z = np.load(OUT_BASELINE)
+        meta = json.loads(str(z["meta"]))
+        data = {k: z[k] for k in z.files if k not in ("meta", "computed")}
+        for f in sys.argv[2:]:
+            z = np.load(f)
+            for name in json.loads(str(z["computed"])):
+                meta[name] = json.loads(str(z["meta"]))[name]
+                data.update({k: z[k] for k in z.files if k.startswith(name + "_")})
+        data["meta"] = np.array(json.dumps(meta))
+        np.savez_compressed(OUT_BASELINE, **data)
+        print("wrote", OUT_BASELINE)
     else:
         main()

@@ -35,9 +35,9 @@ visiting order stays the scene order.  literal=True switches the estimate off (t
 checks both agree).
 
 The RNG is the declared substitution (rt_device.hpp): the reference's thread_rng()
-cannot be seeded, so every build keys Philox4x32-10 by (sample, pixel, bounce, stream):
-stream 0 (s, pix, 0, 0) camera jitter, stream 1 (s, pix, i, 1) disk try i, stream 2 (s, pix, k, 2)
-the scatter at bounce k (random_unit_vector from (u1, u2) as z = 1-2 u1, phi = 2 pi u2 with the
+cannot be seeded, so every build keys Philox4x32-10 (fp32: Philox2x32-10, see uniforms) by (sample,
+pixel, bounce, stream): stream 0 (s, pix, 0, 0) camera jitter, stream 1 (s, pix, i, 1) disk try i,
+stream 2 (s, pix, k, 2) the scatter at bounce k (random_unit_vector from (u1, u2) as z = 1-2 u1, phi = 2 pi u2 with the
 fixed fma-Horner sin/cos; the Dielectric draw is u1).  Philox itself is restated from Random123's
 spec and checked against its published KAT vectors (tests/test_independent_v2.py).
 """
@@ -212,12 +212,27 @@ def philox4x32_10(ctr, key):
     return (c0, c1, c2, c3)
 
 
+def philox2x32_10(ctr, key):
+    """Random123 Philox2x32 with 10 rounds: hi:lo = 0xD256D193 * c0, (c0, c1) <- (hi ^ key ^ c1, lo), then
+    bump the key by the Weyl constant 0x9E3779B9."""
+    c0, c1 = ctr
+    for _ in range(10):
+        p = 0xD256D193 * c0
+        c0, c1 = ((p >> 32) ^ key ^ c1) & _M, p & _M
+        key = (key + 0x9E3779B9) & _M
+    return (c0, c1)
+
+
 def uniforms(sid, pix, k, stream, seed, prec="f64"):
-    """Two uniforms in [0, 1): f64 from 53 bits of (r0, r1) and of (r2, r3); fp32 from 24 bits of r0 and
-    of r1."""
-    r = philox4x32_10((sid, pix, k, stream), (seed & _M, (seed >> 32) & _M))
+    """Two uniforms in [0, 1): f64 from 53 bits of (r0, r1) and of (r2, r3) of Philox4x32-10 at counter
+    (sid, pix, k, stream), key (seed lo, seed hi); fp32 from 24 bits of each word of Philox2x32-10 at
+    counter (pix, sid | code << 20), code 0 camera / 1 + k disk try / 257 + k scatter, key seed lo ^ hi."""
     if prec == "f32":
+        code = 0 if stream == 0 else (1 + k if stream == 1 else 257 + k)
+        assert sid < (1 << 20) and code < (1 << 12)
+        r = philox2x32_10((pix, sid | (code << 20)), (seed & _M) ^ ((seed >> 32) & _M))
         return F32((r[0] >> 8) * 2.0 ** -24), F32((r[1] >> 8) * 2.0 ** -24)
+    r = philox4x32_10((sid, pix, k, stream), (seed & _M, (seed >> 32) & _M))
     ua = (((r[0] << 32) | r[1]) >> 11) * 2.0 ** -53
     ub = (((r[2] << 32) | r[3]) >> 11) * 2.0 ** -53
     return ua, ub

@@ -38,6 +38,7 @@ def load_oracle(path=None):
     lib.oracle_camera_new.argtypes = [vp, u32, u32, f64, f64, ctypes.POINTER(f64), ctypes.POINTER(f64),
                                       ctypes.POINTER(f64), f64]
     lib.oracle_philox4x32_10.argtypes = [ctypes.POINTER(u32), ctypes.POINTER(u32), ctypes.POINTER(u32)]
+    lib.oracle_philox2x32_10.argtypes = [ctypes.POINTER(u32), u32, ctypes.POINTER(u32)]
     lib.oracle_sincos2pi_f64.argtypes = [f64, ctypes.POINTER(f64), ctypes.POINTER(f64)]
     lib.oracle_to_u8.argtypes = [ctypes.POINTER(f64), ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_int)]
     lib.oracle_get_ray_f64.argtypes = [vp, u32, u32, u32, u64, ctypes.POINTER(f64), ctypes.POINTER(f64)]

@@ -44,10 +44,13 @@ def spot_check(flat, cam, depth, spp, lin, rows, n_spot, precision):
 
 # ---------------------------------------------------------------- fp32 against fp64 at config C
 def test_fp32_tracks_fp64_at_config_c(renderer):
-    """north_star's stated fp32 tolerance, at the benched size (config C, 1920x1080, 512 spp): the
-    fp32 frame against the fp64 frame of the same seed (same RNG keys, so the two differ only where
-    rounding flips a path) must have (1) every channel's image mean within 0.5 % and (2) a per-pixel
-    RMSE below the Monte-Carlo noise, measured as the RMSE between two fp64 frames of different seeds."""
+    """north_star's stated fp32 tolerance, at the benched size (config C, 1920x1080, 512 spp).  fp32 draws
+    its own Philox2x32 stream (rt_device.hpp rng<T>), so the fp32 frame is an independent estimate of the
+    image the fp64 frame estimates: (1) every channel's image mean within 0.5 % of the fp64 frame's, and
+    (2) its per-pixel differences from the fp64 frame no larger than those of an fp64 frame of another
+    seed (a bias of the fp32 arithmetic would add to them): median |difference| within 3 % and RMSE within
+    5 % of the fp64 seed-to-seed values (two million pixels: both ratios of unbiased estimates stay within
+    about 1 %)."""
     w, h, _, spp, depth = rt.scenes.CONFIGS["C"]
     flat = rt.scenes.config_scene("C").flatten()
     cam = cam_for(w, h)
@@ -58,10 +61,12 @@ def test_fp32_tracks_fp64_at_config_c(renderer):
     assert np.all(np.abs(m32 / m64 - 1.0) < 0.005), (m32, m64)
     rmse = float(np.sqrt(np.mean((l32 - l64) ** 2)))
     noise = float(np.sqrt(np.mean((l64b - l64) ** 2)))
-    assert rmse < noise, (rmse, noise)
-    # recorded by the run (pytest -s): how far below the noise the precision difference is
+    med = float(np.median(np.abs(l32 - l64)) / np.median(np.abs(l64b - l64)))
+    assert rmse < 1.05 * noise, (rmse, noise)
+    assert 0.97 < med < 1.03, med
+    # recorded by the run (pytest -s)
     print(f"config C: fp32/fp64 channel means {m32 / m64}, rmse fp32-fp64 {rmse:.3e}, "
-          f"fp64 seed-to-seed {noise:.3e}, pixels differing {np.mean((l32 != l64).any(axis=1)):.4f}")
+          f"fp64 seed-to-seed {noise:.3e}, median |diff| ratio {med:.4f}")
 
 
 # ---------------------------------------------------------------- fp64 at the BASELINE sizes

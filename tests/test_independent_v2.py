@@ -46,6 +46,13 @@ def test_philox_published_kats():
         (0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1)
 
 
+def test_philox2x32_published_kats():
+    """Random123 kat_vectors, philox2x32 R=10 (the fp32 draws; restated from the spec, not from the oracle)."""
+    assert iv.philox2x32_10((0, 0), 0) == (0xFF1DAE59, 0x6CD10DF2)
+    assert iv.philox2x32_10((0xFFFFFFFF, 0xFFFFFFFF), 0xFFFFFFFF) == (0x2C3F628B, 0xAB4FD7AD)
+    assert iv.philox2x32_10((0x243F6A88, 0x85A308D3), 0x13198A2E) == (0xDD7CE038, 0xF62A4C12)
+
+
 def test_exact_fma():
     """iv.fma is the correctly rounded a*b+c (checked against Fraction arithmetic)."""
     rng = random.Random(7)

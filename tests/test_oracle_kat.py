@@ -36,6 +36,31 @@ def test_philox_published_kats():
         [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
 
 
+def philox2(ctr, key):
+    lib = load_oracle()
+    out = (ctypes.c_uint32 * 2)()
+    lib.oracle_philox2x32_10((ctypes.c_uint32 * 2)(*ctr), ctypes.c_uint32(key), out)
+    return list(out)
+
+
+def test_philox2x32_published_kats():
+    # Random123 kat_vectors, philox2x32 R=10 (the fp32 build's draws, rt_device.hpp rng<float>)
+    assert philox2([0, 0], 0) == [0xFF1DAE59, 0x6CD10DF2]
+    assert philox2([0xFFFFFFFF] * 2, 0xFFFFFFFF) == [0x2C3F628B, 0xAB4FD7AD]
+    assert philox2([0x243F6A88, 0x85A308D3], 0x13198A2E) == [0xDD7CE038, 0xF62A4C12]
+
+
+def test_f32_rng_limits():
+    """fp32's counter (pixel, sample | code << 20) holds spp <= 2^20 and 257 + bounce < 2^12: the oracle,
+    like rt_render (RT_MAX_BOUNCES_F32, RT_ERR_UNSUPPORTED), refuses larger configurations with 4."""
+    flat = rt.scenes.config_scene("A").flatten()
+    cam = rt.camera_new_py(2, 2, **rt.MAIN_CAMERA)
+    assert oracle_render(flat, cam, 3839, 4, SEED, precision="f32")[3] == 0
+    assert oracle_render(flat, cam, 3840, 4, SEED, precision="f32")[3] == 4
+    assert oracle_render(flat, cam, 3840, 4, SEED, precision="f64")[3] == 0
+    assert abi.RT_MAX_BOUNCES_F32 == 3839
+
+
 def test_camera_new_kat():
     """Camera::new for src/main.rs:51-58 at 16:9 (ray_tracing.rs:27-62), hand-derived values."""
     lib = load_oracle()
@@ -195,18 +220,23 @@ def test_pixel_subset_matches_full():
 
 
 def test_fp32_tracks_fp64_statistically():
-    """fp32 mode vs the reference's fp64 arithmetic: per-channel image mean within 0.5 % and
-    per-pixel RMSE below the Monte-Carlo noise of the fp64 image (the fp32 tolerance we state)."""
+    """fp32 mode vs the reference's fp64 arithmetic (the fp32 tolerance we state): fp32 draws its own
+    Philox2x32 stream, so an fp32 frame is an independent estimate of the same image.  Per-channel image
+    means within 0.5 %, and its per-pixel differences from an fp64 frame no larger than an independent fp64
+    frame's (a bias in the fp32 arithmetic would add to them): median |difference| within 10 % and RMSE
+    within 15 % of the fp64 seed-to-seed values (heavy-tailed pixels: at 96x54 and 64 spp the ratios of two
+    unbiased estimates scatter by about +-3 % and +-8 %)."""
     flat = rt.scenes.random_spheres(500).flatten()
-    cam = rt.camera_new_py(48, 27, **rt.MAIN_CAMERA)
+    cam = rt.camera_new_py(96, 54, **rt.MAIN_CAMERA)
     _, l64, _, _ = oracle_render(flat, cam, 50, 64, SEED)
     _, l32, _, _ = oracle_render(flat, cam, 50, 64, SEED, precision="f32")
     _, l64b, _, _ = oracle_render(flat, cam, 50, 64, SEED + 1)
     m64, m32 = l64.mean(0), l32.mean(0)
     assert np.all(np.abs(m32 - m64) / m64 < 5e-3)
-    rmse = np.sqrt(((l32 - l64) ** 2).mean())
-    noise = np.sqrt(((l64b - l64) ** 2).mean())   # two independent fp64 renders
-    assert rmse < noise
+    med = np.median(np.abs(l32 - l64)) / np.median(np.abs(l64b - l64))
+    rmse = np.sqrt(((l32 - l64) ** 2).mean()) / np.sqrt(((l64b - l64) ** 2).mean())
+    assert 0.9 < med < 1.1, med
+    assert rmse < 1.15, rmse
 
 
 @pytest.mark.parametrize("name", sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith(".npz") and not f.startswith("independent")))

@@ -7,8 +7,9 @@ substitution must preserve is each draw's DISTRIBUTION:
   * Vec3::random_unit_vector (geometry.rs:139-152): a normalised 3-D standard normal, i.e.
     uniform on S^2                                                   -> unit_vec(u1, u2)
   * Vec3::random_in_unit_disk (geometry.rs:154-168): rejection on [-1,1]^2 -> uniform on the disk
-These tests draw from the same Philox4x32-10 words and the same polynomial sin/cos as the
-oracle and the kernel, and compare moments and histograms with the exact distributions.
+These tests draw from the same Philox4x32-10 words (fp64) and Philox2x32-10 words (fp32) and the same
+polynomial sin/cos as the oracle and the kernel, and compare moments and histograms with the exact
+distributions.
 """
 import ctypes
 import math
@@ -119,3 +120,39 @@ def test_disk_rejection_is_uniform_on_disk():
     assert ((hist - n / 10) ** 2 / (n / 10)).sum() < 30.0
     ang = np.histogram(np.arctan2(p[:, 1], p[:, 0]), bins=12, range=(-math.pi, math.pi))[0]
     assert ((ang - n / 12) ** 2 / (n / 12)).sum() < 35.0
+
+
+def _blocks2(n, code, pix=12345):
+    """fp32 draws: Philox2x32-10 at counter (pixel, sample | code << 20), key seed lo ^ seed hi."""
+    lib = load_oracle()
+    out = np.zeros((n, 2), np.uint64)
+    o = (ctypes.c_uint32 * 2)()
+    key = ctypes.c_uint32((SEED & 0xFFFFFFFF) ^ (SEED >> 32))
+    for s in range(n):
+        lib.oracle_philox2x32_10((ctypes.c_uint32 * 2)(pix, s | (code << 20)), key, o)
+        out[s] = list(o)
+    return out
+
+
+def test_f32_uniform_draws():
+    """The fp32 build's two 24-bit uniforms per block (camera, scatter at bounces 0 and 49): uniform, and
+    independent of each other and of the neighbouring streams."""
+    bs = [_blocks2(N, code) for code in (0, 257, 257 + 49)]
+    us = []
+    for b in bs:
+        for w in (0, 1):
+            u = (b[:, w] >> np.uint64(8)).astype(np.float64) * 2.0 ** -24
+            assert u.min() >= 0.0 and u.max() < 1.0
+            assert abs(u.mean() - 0.5) < 4 * math.sqrt(1 / 12 / N)
+            hist = np.histogram(u, bins=20, range=(0, 1))[0]
+            assert ((hist - N / 20) ** 2 / (N / 20)).sum() < 45.0
+            us.append(u)
+    c = np.corrcoef(np.stack(us))
+    assert np.all(np.abs(c - np.eye(len(us))) < 4 / math.sqrt(N))
+    # the unit vector from an fp32 block: every coordinate uniform on [-1, 1]
+    b = bs[1]
+    v = _unit_vec((b[:, 0] >> np.uint64(8)).astype(np.float64) * 2.0 ** -24,
+                  (b[:, 1] >> np.uint64(8)).astype(np.float64) * 2.0 ** -24)
+    for k in range(3):
+        hist = np.histogram(v[:, k], bins=20, range=(-1, 1))[0]
+        assert ((hist - N / 20) ** 2 / (N / 20)).sum() < 45.0
