@@ -359,7 +359,7 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         if constexpr (SCALAR) rad = sg[3];
         l2 = pk_len2(vec);
     }
-    const T len = (SCALAR && !cam) ? rad : sqrt(l2);
+    const T len = (SCALAR && !cam) ? rad : sqrt_len(l2);
     const V3<T> u = dvs(vec, len);
     if (cam) {
         o = base;

@@ -52,10 +52,45 @@ __device__ __forceinline__ float sqrt_nd(float x) {
     return r;
 }
 __device__ __forceinline__ double sqrt_nd(double x) { return sqrt(x); }
+// fp64 a / s, s > 0, for three components: the compiler's f64 division (div_scale x2, rcp, two Newton steps,
+// the residual FMA, div_fmas, div_fixup) where div_scale scales nothing and div_fixup has nothing to fix
+// (every lane: 2^-20 <= s <= 2^20 and every |a_i| >= 2^-100): the same operations, the reciprocal shared.
+template <> __device__ __forceinline__ V3<double> dvs(V3<double> a, double s) {
+    const double mn = fmin(fmin(fabs(a.x), fabs(a.y)), fabs(a.z));
+    const bool ok = s >= 0x1.0p-20 && s <= 0x1.0p20 && mn >= 0x1.0p-100;
+    if (__builtin_expect(__ballot(!ok) == 0ull, 1)) {
+        double r = __builtin_amdgcn_rcp(s);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+        r = __builtin_fma(r, __builtin_fma(-s, r, 1.0), r);
+        auto q = [&](double x) {
+            const double m = x * r;
+            return __builtin_fma(__builtin_fma(-s, m, x), r, m);
+        };
+        return mk(q(a.x), q(a.y), q(a.z));
+    }
+    return mk(a.x / s, a.y / s, a.z / s);
+}
+// sqrt(x), x = |v|^2 of a direction: the compiler's f64 sqrt (rsq, then Goldschmidt/Newton refinement) without
+// its ldexp scaling for x < 2^-767 and its select for zero / inf, when every lane has 2^-100 <= x <= 2^100.
+__device__ __forceinline__ double sqrt_len(double x) {
+    if (__builtin_expect(__ballot(!(x >= 0x1.0p-100 && x <= 0x1.0p100)) == 0ull, 1)) {
+        const double g0 = __builtin_amdgcn_rsq(x);
+        double sq = x * g0, h = g0 * 0.5;
+        const double r = __builtin_fma(-h, sq, 0.5);
+        sq = __builtin_fma(sq, r, sq);
+        const double d0 = __builtin_fma(-sq, sq, x);
+        h = __builtin_fma(h, r, h);
+        sq = __builtin_fma(d0, h, sq);
+        const double d1 = __builtin_fma(-sq, sq, x);
+        return __builtin_fma(d1, h, sq);
+    }
+    return sqrt(x);
+}
+__device__ __forceinline__ float sqrt_len(float x) { return sqrtf(x); }
 template <typename T> __device__ __forceinline__ V3<T> neg(V3<T> a) { return mk(-a.x, -a.y, -a.z); }
 template <typename T> __device__ __forceinline__ T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 template <typename T> __device__ __forceinline__ T len2(V3<T> a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
-template <typename T> __device__ __forceinline__ V3<T> unit(V3<T> a) { return dvs(a, sqrt(len2(a))); }
+template <typename T> __device__ __forceinline__ V3<T> unit(V3<T> a) { return dvs(a, sqrt_len(len2(a))); }
 // Packed ops keep the reference's explicit FMA.
 template <typename T> __device__ __forceinline__ T pk_len2(V3<T> a) { return fma(a.z, a.z, fma(a.y, a.y, a.x * a.x)); }
 template <typename T> __device__ __forceinline__ T pk_dot(V3<T> a, V3<T> b) { return fma(a.z, b.z, fma(a.y, b.y, a.x * b.x)); }
