@@ -12,7 +12,7 @@
  *     cannot be built here (Rust nightly + crates.io deps; no rustc/cargo).
  *   - The reference draws from rand::thread_rng() (unseedable ChaCha12, rand 0.8.5)
  *     and rand_distr 0.4.3 Normal; those streams cannot be reproduced.  This oracle
- *     substitutes a keyed Philox4x32-10 stream with the same distributions
+ *     substitutes keyed Philox4x32-10 (f64) and Philox2x32-10 (f32) streams with the same distributions
  *     (see oracle_impl.h "RNG boundary").
  *   - What IS pinned: every deterministic formula (camera, sphere test, hit-record
  *     finalize, scatter, compaction, sky, final buffer read, quantization) follows

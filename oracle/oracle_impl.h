@@ -10,7 +10,7 @@
  * geometry.rs:105-188, have none).
  *
  * RNG boundary (parity unpinned, see oracle.h):  every random draw is a pure
- * function of (seed, pixel, sample, bounce, stream) through Philox4x32-10, so
+ * function of (seed, pixel, sample, bounce, stream) through Philox4x32-10 (f64; f32: Philox2x32-10, SFX(draw) below), so
  * results do not depend on threading, compaction order or GPU count.
  *   stream 0, ctr (s, pix, 0, 0): Camera::get_ray jitter      (ray_tracing.rs:78-79)
  *   stream 1, ctr (s, pix, i, 1): random_in_unit_disk try i  (geometry.rs:154-168)
