@@ -317,6 +317,14 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
 template <typename T, bool SCALAR>
 __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy, uint32_t pix, uint32_t sid,
                                          uint32_t k, int hit_i, T hit_t, V3<T>& o, V3<T>& d, V3<T>& c) {
+    // the hit sphere's centre and material, requested before the draw (scatter lanes; a camera lane reads
+    // record 0, unused)
+    const int hg = cam ? 0 : hit_i;
+    const auto& qg = *cold_args<T>();
+    const T* sgp = qg.cen + 4 * hg;
+    const V3<T> hcen = mk(sgp[0], sgp[1], sgp[2]);
+    const T hrad = sgp[3];
+    const MatT<T> m = qg.mats[hg];                       // = materials[material[hit_i]] (objects.rs:296)
     const U4 r = [&] {
         const auto& q0 = *cold_args<T>();
         return rng<T>(sid, pix, cam ? 0u : k, cam ? 0u : 2u, q0.k0, q0.k1);
@@ -354,9 +362,8 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
         l2 = len2(vec);                                   // unit(): Vec3::length (geometry.rs:106-112)
     } else {
         base = mk(o.x + d.x * hit_t, o.y + d.y * hit_t, o.z + d.z * hit_t);   // at_t
-        const T* sg = q.cen + 4 * hit_i;
-        vec = sub(base, mk(sg[0], sg[1], sg[2]));        // normal = at_t(t) - center (objects.rs:279-280)
-        if constexpr (SCALAR) rad = sg[3];
+        vec = sub(base, hcen);                           // normal = at_t(t) - center (objects.rs:279-280)
+        if constexpr (SCALAR) rad = hrad;
         l2 = pk_len2(vec);
     }
     const T len = (SCALAR && !cam) ? rad : sqrt_len(l2);
@@ -370,7 +377,6 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
     V3<T> nrm = u;
     const bool front = (SCALAR ? dot(d, nrm) : pk_dot(d, nrm)) < T(0.0);
     if (!front) nrm = neg(nrm);
-    const MatT<T> m = q.mats[hit_i];                     // = materials[material[hit_i]] (objects.rs:296)
     V3<T> nd;
     if (m.kind != RT_DIELECTRIC) {
         // One random_unit_vector for both kinds (a wave usually holds both: one evaluation, not two).
