@@ -157,8 +157,11 @@ __device__ __forceinline__ T reduce_positions(uint32_t P, uint32_t* hist, T (*st
 // position map (LDS or the wave's scratch): the same values and the same order of adds as
 // reduce_positions with finish_pixel's generic value lambda (the partial last batch, spp % 64, goes through
 // that lambda), specialised: no bounds test in whole batches, a three-op map decode, a branch-free record
-// load for positions without an entry (clamped to a valid record, value 0), the y load independent of the
-// map, the next batch's map entry loaded before this batch's records, and the 12 running sums in a VGPR.
+// load for positions without an entry (clamped to a valid record, value 0), the 12 running sums in a VGPR,
+// and two batches per iteration: the y, map and record loads of both are issued together and the batches
+// staged and summed one after the other, so a 512-position pixel waits for 4 load round trips, not 8
+// (round 5, same-box C fp32 +0.4 %, fp64 +0.6 %, E +0.6 %; prefetching the next pair's map entries as well
+// lost, profiles/r05/reduce_pair_ab.txt).
 template <typename T, typename G>
 __device__ __forceinline__ T reduce_live16(const PScratch<T>& sc, uint32_t s, uint32_t spp, uint32_t P, const uint16_t* lmap,
                                            bool lm, uint32_t* hist, T (*stage)[64], G&& generic) {
@@ -169,19 +172,18 @@ __device__ __forceinline__ T reduce_live16(const PScratch<T>& sc, uint32_t s, ui
     const uint32_t nfull = spp & ~63u;
     const uint16_t* gmap = (const uint16_t*)sc.base;
     const uint32_t si = 16u * (lane & 3u) + (lane >> 2);
-    uint32_t m16n = nfull ? (lm ? (uint32_t)lmap[lane] : (uint32_t)gmap[lane]) : 0xFFFFu;
-    for (uint32_t qb = 0; qb < nfull; qb += 64u) {
-        const uint32_t qq = qb + lane;
-        const T y = sc.y(s, qq);
-        const uint32_t m16 = m16n;
-        if (qb + 64u < nfull) m16n = lm ? (uint32_t)lmap[qq + 64u] : (uint32_t)gmap[qq + 64u];
+    auto mapat = [&](uint32_t qi) -> uint32_t { return lm ? (uint32_t)lmap[qi] : (uint32_t)gmap[qi]; };
+    // values of one batch (positions qb + lane) from its y, map entry and record
+    auto vals16 = [&](T y, uint32_t m16, const C3<T>& cm, T& vr, T& vg, T& vb) {
         const bool has = m16 != 0xFFFFu, wh = m16 >= 0x8000u;
-        const uint32_t smp = min(m16 & 0x7FFFu, spp - 1u);   // a clamped (unused) record without an entry
-        const C3<T> cm = sc.c(s, smp);
         const V3<T> sk = sky(y);
-        const T vr = has ? (wh ? sk.x : cm.x * sk.x) : T(0.0);   // (white x sky) == sky, bit for bit
-        const T vg = has ? (wh ? sk.y : cm.y * sk.y) : T(0.0);
-        const T vb = has ? (wh ? sk.z : cm.z * sk.z) : T(0.0);
+        vr = has ? (wh ? sk.x : cm.x * sk.x) : T(0.0);   // (white x sky) == sky, bit for bit
+        vg = has ? (wh ? sk.y : cm.y * sk.y) : T(0.0);
+        vb = has ? (wh ? sk.z : cm.z * sk.z) : T(0.0);
+    };
+    auto rec = [&](uint32_t m16) -> C3<T> { return sc.c(s, min(m16 & 0x7FFFu, spp - 1u)); };   // clamped when none
+    // the 12 lanes' running sums over one staged batch, in position order
+    auto sum16 = [&](T vr, T vg, T vb) {
         stage[0][si] = vr; stage[1][si] = vg; stage[2][si] = vb;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_wave_barrier();
@@ -199,6 +201,24 @@ __device__ __forceinline__ T reduce_live16(const PScratch<T>& sc, uint32_t s, ui
             racc = a;
         }
         __builtin_amdgcn_wave_barrier();
+    };
+    uint32_t qb = 0;
+    for (; qb + 128u <= nfull; qb += 128u) {   // two batches per round trip
+        const uint32_t qq = qb + lane;
+        const uint32_t m0 = mapat(qq), m1 = mapat(qq + 64u);
+        const T y0 = sc.y(s, qq), y1 = sc.y(s, qq + 64u);
+        const C3<T> c0 = rec(m0), c1 = rec(m1);
+        T r0, g0, b0, r1, g1, b1;
+        vals16(y0, m0, c0, r0, g0, b0);
+        vals16(y1, m1, c1, r1, g1, b1);
+        sum16(r0, g0, b0);
+        sum16(r1, g1, b1);
+    }
+    if (qb < nfull) {   // a leftover single batch
+        const uint32_t qq = qb + lane, m0 = mapat(qq);
+        T r0, g0, b0;
+        vals16(sc.y(s, qq), m0, rec(m0), r0, g0, b0);
+        sum16(r0, g0, b0);
     }
     if (lane < 12u) accl[lane] = racc;
     // the partial last batch (and positions past spp): the generic path, continuing the same sums
