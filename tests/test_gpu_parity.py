@@ -126,6 +126,17 @@ def test_spp_limit(renderer, scene_100):
     assert e.value.code == abi.RT_ERR_UNSUPPORTED
 
 
+def test_f32_bounce_limit(renderer, scene_100):
+    """fp32 draws Philox2x32 with the counter (pixel, sample | (257 + bounce) << 20): max_bounces up to
+    RT_MAX_BOUNCES_F32 renders (bit-exact against the oracle, which has the same limit), one more is
+    RT_ERR_UNSUPPORTED; fp64 (Philox4x32, the bounce in its own word) has no such limit."""
+    assert_parity(renderer, scene_100, cam_for(2, 1), abi.RT_MAX_BOUNCES_F32, 8, abi.RT_FLAG_F32)
+    with pytest.raises(rt.RtError) as e:
+        gpu(renderer, scene_100, cam_for(2, 1), abi.RT_MAX_BOUNCES_F32 + 1, 8, flags=abi.RT_FLAG_F32)
+    assert e.value.code == abi.RT_ERR_UNSUPPORTED
+    assert_parity(renderer, scene_100, cam_for(2, 1), abi.RT_MAX_BOUNCES_F32 + 1, 8, 0)
+
+
 def test_tile_ranges_compose(renderer, scene_100):
     """Row-interleaved shards (the multi-GPU partition) reassemble the full image bit-exactly."""
     cam = cam_for(64, 36)
