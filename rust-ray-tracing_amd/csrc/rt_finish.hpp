@@ -292,7 +292,7 @@ __device__ __forceinline__ void finish_sky_direct(uint32_t item, uint32_t col, u
 // The position map in LDS (live-path kernels without the mega level, P <= kLMapCap positions: config C's
 // 512 spp): the replay's scattered u16 writes, the map's initialisation and the reduction's reads stay
 // on the CU instead of going to HBM as partial lines.  Larger P uses the global map in PScratch.
-template <typename T, int MODE>
+template <typename T, int MODE, bool BALLOT01 = true>
 __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t s, uint32_t item, uint32_t* hist,
                                                  T (*stage)[64], uint16_t* lmap, bool all_e0 = false) {
     const auto& q = *cold_args<T>();
@@ -319,7 +319,11 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
     }
     if (known1) K = 1u;
     else if (depth > 0) {
-        uint32_t me = 0;
+        // BALLOT01: the two commonest bounces (e = 0, the sky at bounce 0: 43 % of config C's samples; e = 1)
+        // are counted with ballots into wave-uniform sums, LDS atomics only for e >= 2 (64 lanes adding to one
+        // LDS word serialise): C fp32 +0.4 %, fp64 +0.1 %; the mega kernels (config E, fewer bounce-0 skies)
+        // lost 0.3 % and keep the atomics (profiles/r05/hist01_ab.txt)
+        uint32_t me = 0, h0 = 0, h1 = 0;   // #{e == 0}, #{e == 1} (wave-uniform)
         for (uint32_t b = 0; b < spp; b += 512u) {
             uint32_t ev[8];
 #pragma unroll
@@ -330,10 +334,23 @@ __device__ __forceinline__ uint32_t finish_pixel(const PScratch<T>& sc, uint32_t
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 me = max(me, ev[u]);
-                if (hist_on && b + 64u * u + lane < spp && ev[u] < depth && ev[u] < 64u) atomicAdd(&hist[ev[u]], 1u);
+                const bool hk = hist_on && b + 64u * u + lane < spp && ev[u] < depth && ev[u] < 64u;
+                if constexpr (BALLOT01) {
+                    h0 += (uint32_t)__popcll(__ballot(hk && ev[u] == 0u));
+                    h1 += (uint32_t)__popcll(__ballot(hk && ev[u] == 1u));
+                    if (hk && ev[u] >= 2u) atomicAdd(&hist[ev[u]], 1u);
+                } else if (hk) {
+                    atomicAdd(&hist[ev[u]], 1u);
+                }
             }
         }
         K = min(depth, __builtin_amdgcn_readfirstlane(wave_max(me)) + 1u);
+        if (BALLOT01 && hist_on) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0u) hist[0] = h0;
+            if (lane == 1u) hist[1] = h1;
+        }
     }
     // Sky pixels: K = 1 with depth > 1 means every sample hit the sky at bounce 0 (e = 0 < depth), so
     // the replay is the identity (bounce 0 retires every position: lo = 0, and pold = pnew = i) and

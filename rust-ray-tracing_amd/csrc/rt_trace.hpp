@@ -320,7 +320,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
                 const uint32_t ss_keep = kParkSS ? *ssp : 0u;   // finish_pixel overwrites the stage
                 if (!synced) { wave_mem_sync(); synced = true; }
                 KSTAT(6);
-                const uint32_t K = finish_pixel<T, MODE>(
+                const uint32_t K = finish_pixel<T, MODE, !MEGA>(
                     wave_scratch<T>(wave), s, __builtin_amdgcn_readfirstlane(s_item[wave][s]), s_hist[wave], s_stage[wave],
                     kLMap ? s_lmap[wave] : nullptr, (left & kSlotNZ) == 0u);
                 if constexpr (kParkSS) {
