@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256, W) void trace_paths(KParams<T> p) {
     __shared__ int q_hit[QW][QN];
     __shared__ T q_t[QW][QN], q_d[QW][3][QN];
     // camera candidate list of each open pixel slot (pixel_list): [0] = count (0xFFFF: none, sweep per batch)
-    __shared__ uint16_t s_clist[QW][CAMQ ? kSlots : 1][kCList];
+    __shared__ alignas(16) uint16_t s_clist[QW][CAMQ ? kSlots : 1][kCList];   // 16 B lists: one LDS read (fp64)
     // fp32 at 6 waves per SIMD (80 VGPRs): each lane's ray origin and direction are parked in LDS
     // across the sphere sweeps and the camera batches and re-read right before the scatter, instead
     // of being held in VGPRs (the allocator otherwise spills them to scratch memory around the sweep).
