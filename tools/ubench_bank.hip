@@ -104,6 +104,21 @@ __global__ __launch_bounds__(256) void bank(float* out, int iters) {
 #define X(j) "v_fma_f64 v[44+2*" #j ":45+2*" #j "], v[42:43], v[40:41], v[44+2*" #j ":45+2*" #j "]\n"
                 R16(X) ::: CLOB);
 #undef X
+        if constexpr (K == 16)   // compare into VCC (VOP2/VOPC encoding)
+            asm volatile(
+#define X(j) "v_cmp_lt_f32_e32 vcc, v41, v[44+2*" #j "]\n"
+                R16(X) ::: CLOB, "vcc");
+#undef X
+        if constexpr (K == 17)   // compare into VCC, then a select on it (the pair, one instruction each)
+            asm volatile(
+#define X(j) "v_cmp_lt_f32_e32 vcc, v41, v[44+2*" #j "]\n v_cndmask_b32_e32 v[45+2*" #j "], v41, v[45+2*" #j "], vcc\n"
+                R16(X) ::: CLOB, "vcc");
+#undef X
+        if constexpr (K == 18)   // compare into an SGPR pair, then a select on it
+            asm volatile(
+#define X(j) "v_cmp_lt_f32_e64 s[20+2*(" #j "&3):21+2*(" #j "&3)], v41, v[44+2*" #j "]\n v_cndmask_b32_e64 v[45+2*" #j "], v41, v[45+2*" #j "], s[20+2*(" #j "&3):21+2*(" #j "&3)]\n"
+                R16(X) ::: CLOB, "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+#undef X
     }
     float r;
     asm volatile("v_mov_b32 %0, v44" : "=v"(r)::CLOB);
@@ -112,7 +127,8 @@ __global__ __launch_bounds__(256) void bank(float* out, int iters) {
 
 static const char* names[] = {"fma b1,b3,acc", "fma x*x+acc", "fma b0,b0,acc", "pk_fma distinct", "pk_fma x*x+acc",
                               "mul x*x", "mul distinct", "fma b0,b1,acc(b0)", "cndmask_e64 sgpr", "cmp_e64",
-                              "mov", "and", "bitop3 distinct", "add_f64", "mul_f64", "fma_f64 distinct"};
+                              "mov", "and", "bitop3 distinct", "add_f64", "mul_f64", "fma_f64 distinct",
+                              "cmp_e32 vcc", "cmp_e32+cndmask_e32 (2)", "cmp_e64+cndmask_e64 (2)"};
 template <int K>
 static void run() {
     const int blocks = 256 * 8, threads = 256, iters = 8192;
@@ -138,5 +154,6 @@ int main() {
     for (int w = 0; w < 3; ++w) run<0>();
     run<0>(); run<1>(); run<2>(); run<3>(); run<4>(); run<5>(); run<6>(); run<7>();
     run<8>(); run<9>(); run<10>(); run<11>(); run<12>(); run<13>(); run<14>(); run<15>();
+    run<16>(); run<17>(); run<18>();
     return 0;
 }

@@ -32,8 +32,11 @@ def counters(prec):
 
 
 # SIMD-cycles per wave-instruction (ubench_mix / ubench_bank, warm clocks, 2.4 GHz)
-COST = {"FMA_F32_scalar": 2.5, "FMA_F32_packed": 4.6, "FMA_F64": 4.6, "ADD_F64": 4.6, "MUL_F64": 4.6,
+COST = {"FMA_F32_scalar": 2.5, "FMA_F32_packed": 4.6, "FMA_F64": 4.3, "ADD_F64": 4.3, "MUL_F64": 4.3,
         "MUL_F32": 2.5, "ADD_F32": 2.5, "TRANS_F32": 8.9, "TRANS_F64": 16.3, "INT32": 2.9, "INT64": 4.5, "CVT": 4.7}
+# "other": moves and logic cost 2.5-2.7, compares (e32 or e64) and selects on a lane mask 4.1-4.7; the C kernel's
+# static code has about as many compares and selects as moves and logic ops, so "other" averages ~3.4: the model
+# brackets it with 3.0 and 3.7 (and prints the extremes 2.5 / 4.4 for reference)
 
 for prec, packed in (("f32", (0.5, 0.9)), ("f64", (0.5, 0.9))):
     c = counters(prec)
@@ -45,13 +48,14 @@ for prec, packed in (("f32", (0.5, 0.9)), ("f64", (0.5, 0.9))):
           + ", ".join(f"{k} {x / v:.3f}" for k, x in sorted(cls.items()) if x) + f", other {other / v:.3f}")
     lo = hi = None
     for pk in packed:
-        for oc in (2.5, 4.4):
+        for oc in (2.5, 3.0, 3.7, 4.4):
             cyc = sum(x * COST[k] for k, x in cls.items() if k != "FMA_F32")
             cyc += cls.get("FMA_F32", 0.0) * (pk * COST["FMA_F32_packed"] + (1 - pk) * COST["FMA_F32_scalar"])
             cyc += other * oc
             b = cyc / simd_cycles
-            lo = b if lo is None else min(lo, b)
-            hi = b if hi is None else max(hi, b)
+            if oc in (3.0, 3.7):
+                lo = b if lo is None else min(lo, b)
+                hi = b if hi is None else max(hi, b)
             print(f"   packed share of FMA_F32 {pk:.1f}, other {oc} cycles: VALU pipe busy {b:.2f}")
     print(f"   {prec}: VALU pipe busy {lo:.2f}-{hi:.2f} of the dispatch's SIMD-cycles; the fma_f32-rate measure "
           f"(valu_busy) reads {v * 2.3 / simd_cycles:.2f}")
