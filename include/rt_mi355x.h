@@ -157,6 +157,10 @@ double rt_metal_clamp_fuzz(double fuzz);
  *   rgb8:   [pixels][3] RGB8, Color::to_u8_array of (sum / spp)   (may be NULL)
  *   linear: [pixels][3] f64 pixel colour after /spp, before gamma (may be NULL)
  *   stats:  may be NULL
+ *   seed:   keys the counter-based draws that replace thread_rng() (ray_tracing.rs:78-79).  fp64
+ *           keys Philox4x32-10 with the whole 64-bit seed.  fp32 (RT_FLAG_F32) keys Philox2x32-10,
+ *           whose key is 32 bits: seed lo ^ fmix32(seed hi) (murmur3's finaliser; fmix32(0) = 0), so
+ *           2^32 seed pairs share each fp32 key, but no structured pattern such as hi == lo does.
  * Returns RT_OK, RT_ERR_RANGE (image written; reference would have panicked) or an error. */
 int rt_render(const rt_scene* scene, const rt_camera* camera, uint32_t max_bounces, uint32_t spp,
               uint64_t seed, uint32_t flags, const rt_tile_range* range, uint8_t* rgb8,

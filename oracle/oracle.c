@@ -49,6 +49,13 @@ void oracle_philox2x32_10(const uint32_t ctr[2], uint32_t key, uint32_t out[2]) 
     out[0] = c0; out[1] = c1;
 }
 
+/* murmur3's 32-bit finaliser (a bijection, fmix32(0) = 0): the fp32 build keys Philox2x32-10 with
+ * seed lo ^ fmix32(seed hi) (rt_device.hpp fmix32), so that the 64-bit seed is not folded by a plain xor. */
+uint32_t oracle_fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
+
 /* ---------------- f64 instantiation (the reference's arithmetic) ---------------- */
 #define REAL double
 #define SFX(x) x##_f64

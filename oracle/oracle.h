@@ -94,6 +94,8 @@ int oracle_camera_new(or_camera* out, uint32_t w, uint32_t h, double focal_lengt
 void oracle_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 /* Philox2x32-10 block: the fp32 build's draws (for KATs). */
 void oracle_philox2x32_10(const uint32_t ctr[2], uint32_t key, uint32_t out[2]);
+/* The fp32 key fold: seed lo ^ oracle_fmix32(seed hi) (murmur3's finaliser). */
+uint32_t oracle_fmix32(uint32_t h);
 
 /* Primitive probes for known-answer tests. */
 void oracle_sincos2pi_f64(double u, double* s, double* c);

@@ -72,7 +72,8 @@ static inline REAL SFX(u01b)(const uint32_t* r) {  /* second independent uniform
 /* One draw block for (sample, pixel, k, stream) (the kernel's rng<T>, rt_device.hpp): stream 0 the camera
  * jitter (k = 0), 1 disk try k, 2 the scatter at bounce k.  f64: Philox4x32-10, counter (sid, pix, k,
  * stream), key (seed lo, seed hi).  f32 uses two 24-bit words only: Philox2x32-10, counter
- * (pix, sid | code << 20) with code 0 / 1 + k / 257 + k, key seed lo ^ seed hi (r[2], r[3] unused). */
+ * (pix, sid | code << 20) with code 0 / 1 + k / 257 + k, key seed lo ^ fmix32(seed hi) (murmur3's
+ * finaliser, oracle_fmix32; r[2], r[3] unused). */
 static inline void SFX(draw)(uint32_t sid, uint32_t pix, uint32_t k, uint32_t stream, uint32_t k0, uint32_t k1,
                              uint32_t r[4]) {
 #if ORACLE_IS_F64
@@ -81,7 +82,7 @@ static inline void SFX(draw)(uint32_t sid, uint32_t pix, uint32_t k, uint32_t st
 #else
     const uint32_t code = stream == 0u ? 0u : (stream == 1u ? 1u + k : 257u + k);
     const uint32_t ctr[2] = {pix, sid | (code << 20)};
-    oracle_philox2x32_10(ctr, k0 ^ k1, r);
+    oracle_philox2x32_10(ctr, k0 ^ oracle_fmix32(k1), r);
     r[2] = 0u; r[3] = 0u;
 #endif
 }

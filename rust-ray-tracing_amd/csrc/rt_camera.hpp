@@ -308,7 +308,8 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
         auto fetch = [&](uint32_t sl) -> CX { return CX{ri[sl], cxt[4 * sl], cxt[4 * sl + 1], cxt[4 * sl + 2], cxt[4 * sl + 3]}; };
         constexpr bool kBothRoots = root2 || SCALAR;
         for (; smask != 0u; smask &= smask - 1u) {
-            const uint4 w = *(const uint4*)lists[__builtin_ctz(smask)];   // the whole list: n, then up to 7 slots
+            uint4 w;   // the whole list: n, then up to 7 slots (memcpy: no type-punned read of the u16 entries)
+            __builtin_memcpy(&w, __builtin_assume_aligned(lists[__builtin_ctz(smask)], 16), sizeof(w));
             const uint32_t w0 = __builtin_amdgcn_readfirstlane(w.x), w1 = __builtin_amdgcn_readfirstlane(w.y),
                            w2 = __builtin_amdgcn_readfirstlane(w.z), w3 = __builtin_amdgcn_readfirstlane(w.w);
             const uint32_t n = w0 & 0xFFFFu;

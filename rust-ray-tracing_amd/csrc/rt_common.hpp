@@ -83,7 +83,7 @@ template <typename T> struct KParams {
     uint32_t row_begin, row_step, col_begin, col_count;
     uint8_t* rgb;
     double* lin;
-    unsigned long long* segs;  // kSegShards counters, one per 128-B line
+    unsigned long long* segs;  // kSegShards shards of kSegStride counters (256 B per shard; direct_sky_samples at slot 16)
     uint32_t* err;
     uint32_t* counter;         // next block of work items (guided_block)
     uint32_t blk_g;            // largest block (a power of two <= kMaxBlock; launch_t)

@@ -136,17 +136,23 @@ __device__ __forceinline__ U4 philox2(uint32_t c0, uint32_t c1, uint32_t k) {
     }
     return U4{c0, c1, 0u, 0u};
 }
+// murmur3's 32-bit finaliser (a bijection with fmix32(0) = 0): folds the seed's high word into the fp32 key.
+__host__ __device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+    return h;
+}
 // One draw block for (sample, pixel, k, stream): stream 0 the camera jitter (k = 0), 1 disk try k, 2 the
 // scatter at bounce k.  fp64 takes two 53-bit uniforms from Philox4x32-10, counter (sample, pixel, k,
-// stream), key (seed lo, seed hi).  fp32 needs only two 24-bit uniforms, so it draws Philox2x32-10 with
-// counter (pixel, sample | code << 20), code = 0 / 1 + k / 257 + k, key seed lo ^ seed hi: half the
-// multiplies (round 5, same-box C fp32 +1.9 %).  The host keeps the counter injective: spp <= 2^20 and,
-// in fp32, max_bounces <= RT_MAX_BOUNCES_F32 (257 + k < 2^12).
+// stream), key (k0, k1) = (seed lo, seed hi).  fp32 needs only two 24-bit uniforms, so it draws
+// Philox2x32-10 with counter (pixel, sample | code << 20), code = 0 / 1 + k / 257 + k, and the 32-bit key
+// k0 = seed lo ^ fmix32(seed hi), folded by the host (launch_t; k1 = 0 unused): half the multiplies (round 5,
+// same-box C fp32 +1.9 %).  The host keeps the counter injective: spp <= 2^20 and, in fp32,
+// max_bounces <= RT_MAX_BOUNCES_F32 (257 + k < 2^12).
 template <typename T>
 __device__ __forceinline__ U4 rng(uint32_t sid, uint32_t pix, uint32_t k, uint32_t stream, uint32_t k0, uint32_t k1) {
     if constexpr (sizeof(T) == 4) {
         const uint32_t code = stream == 0u ? 0u : (stream == 1u ? 1u + k : 257u + k);
-        return philox2(pix, sid | (code << 20), k0 ^ k1);
+        return philox2(pix, sid | (code << 20), k0);
     } else {
         return philox(sid, pix, k, stream, k0, k1);
     }

@@ -527,7 +527,11 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
         if (pinhole) p.flags |= kFlagPinholeInternal;
     }
     p.s_sel = (p.C - 1) % 2;   // ray_tracing.rs:486
-    p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32);
+    // fp64: Philox4x32-10 keyed by (seed lo, seed hi).  fp32: Philox2x32-10 has a 32-bit key, folded here as
+    // seed lo ^ fmix32(seed hi) (rng<float> reads k0 only): fmix32(0) = 0, so a seed below 2^32 keys as itself,
+    // and seeds such as (m << 32) | m no longer all key as 0.
+    if (f64) { p.k0 = (uint32_t)seed; p.k1 = (uint32_t)(seed >> 32); }
+    else { p.k0 = (uint32_t)seed ^ fmix32((uint32_t)(seed >> 32)); p.k1 = 0u; }
     p.row_begin = rg.row_begin; p.row_step = rg.row_step; p.col_begin = rg.col_begin; p.col_count = rg.col_count;
     p.rgb = (uint8_t*)d_rgb;
     p.lin = (double*)d_lin;
@@ -585,12 +589,14 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     // registers) cut its occupancy below the target it was built for (kParkC takes fp32 W6 to 26.8 of the
     // 27.3 KB six workgroups allow): an error, in every build kind, so that neither the product nor an
     // A/B build is ever measured at an occupancy other than the one it names (rt_stats reports both).
-    c->last_kernel_id = pick.id;
-    c->last_wg_per_cu = (uint32_t)per_cu;
+    c->last_kernel_id = 0;   // 0: no kernel (ids have bit 15 set)
+    c->last_wg_per_cu = 0;
     if (per_cu < pick.W)
         return fail(RT_ERR_UNSUPPORTED, std::string(RT_BUILD_KIND) + " build: " + std::to_string(per_cu) +
                                             " workgroups per CU resident, kernel built for " + std::to_string(pick.W) +
                                             " (its LDS or registers grew past the occupancy target)");
+    c->last_kernel_id = pick.id;   // only a kernel that passed the check is ever reported
+    c->last_wg_per_cu = (uint32_t)per_cu;
     uint64_t nblocks = (uint64_t)c->n_cu * (uint64_t)per_cu;
     const uint64_t need = ((uint64_t)p.n_items + 3) / 4;
     if (nblocks > need) nblocks = need;

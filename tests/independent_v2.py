@@ -223,14 +223,24 @@ def philox2x32_10(ctr, key):
     return (c0, c1)
 
 
+def fmix32(h):
+    """murmur3's 32-bit finaliser; the fp32 key is seed lo ^ fmix32(seed hi) (fmix32(0) = 0)."""
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & _M
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & _M
+    return h ^ (h >> 16)
+
+
 def uniforms(sid, pix, k, stream, seed, prec="f64"):
     """Two uniforms in [0, 1): f64 from 53 bits of (r0, r1) and of (r2, r3) of Philox4x32-10 at counter
     (sid, pix, k, stream), key (seed lo, seed hi); fp32 from 24 bits of each word of Philox2x32-10 at
-    counter (pix, sid | code << 20), code 0 camera / 1 + k disk try / 257 + k scatter, key seed lo ^ hi."""
+    counter (pix, sid | code << 20), code 0 camera / 1 + k disk try / 257 + k scatter, key
+    seed lo ^ fmix32(seed hi)."""
     if prec == "f32":
         code = 0 if stream == 0 else (1 + k if stream == 1 else 257 + k)
         assert sid < (1 << 20) and code < (1 << 12)
-        r = philox2x32_10((pix, sid | (code << 20)), (seed & _M) ^ ((seed >> 32) & _M))
+        r = philox2x32_10((pix, sid | (code << 20)), (seed & _M) ^ fmix32((seed >> 32) & _M))
         return F32((r[0] >> 8) * 2.0 ** -24), F32((r[1] >> 8) * 2.0 ** -24)
     r = philox4x32_10((sid, pix, k, stream), (seed & _M, (seed >> 32) & _M))
     ua = (((r[0] << 32) | r[1]) >> 11) * 2.0 ** -53

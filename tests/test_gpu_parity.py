@@ -202,6 +202,18 @@ def test_seed_changes_image(renderer, scene_100):
     np.testing.assert_array_equal(a, c)
 
 
+@pytest.mark.parametrize("seeds", [(0, 0x100000001), (0x5EED0001, 0x5EED0001 ^ (7 << 32) ^ 7),
+                                   (0x1234, 0x1234 << 32)])
+def test_f32_seed_key_uses_all_64_bits(renderer, scene_100, seeds):
+    """fp32 keys Philox2x32 with seed lo ^ fmix32(seed hi) (rt_device.hpp rng<float>): seeds that a plain
+    lo ^ hi fold sends to one key (0 and (1 << 32) | 1; (a, b) and (a ^ m, b ^ m); swapped halves) render
+    different fp32 images, each bit-equal to the oracle's fp32 build."""
+    cam = cam_for(32, 18)
+    a, _ = assert_parity(renderer, scene_100, cam, 50, 8, abi.RT_FLAG_F32, seed=seeds[0])
+    b, _ = assert_parity(renderer, scene_100, cam, 50, 8, abi.RT_FLAG_F32, seed=seeds[1])
+    assert not np.array_equal(a, b)
+
+
 def test_renderer_trait(renderer):
     """GpuRenderer.render mirrors Renderer::render (renderer.rs:38-40)."""
     scene = rt.scenes.three_spheres()

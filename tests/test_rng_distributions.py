@@ -123,11 +123,12 @@ def test_disk_rejection_is_uniform_on_disk():
 
 
 def _blocks2(n, code, pix=12345):
-    """fp32 draws: Philox2x32-10 at counter (pixel, sample | code << 20), key seed lo ^ seed hi."""
+    """fp32 draws: Philox2x32-10 at counter (pixel, sample | code << 20), key seed lo ^ fmix32(seed hi)."""
     lib = load_oracle()
     out = np.zeros((n, 2), np.uint64)
     o = (ctypes.c_uint32 * 2)()
-    key = ctypes.c_uint32((SEED & 0xFFFFFFFF) ^ (SEED >> 32))
+    lib.oracle_fmix32.restype = ctypes.c_uint32
+    key = ctypes.c_uint32((SEED & 0xFFFFFFFF) ^ lib.oracle_fmix32(ctypes.c_uint32(SEED >> 32)))
     for s in range(n):
         lib.oracle_philox2x32_10((ctypes.c_uint32 * 2)(pix, s | (code << 20)), key, o)
         out[s] = list(o)
