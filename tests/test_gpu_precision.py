@@ -195,9 +195,10 @@ def test_config_e_filter_off_same_image(renderer, monkeypatch, flags):
 
 
 def test_launch_size_rule_same_pixels(renderer, monkeypatch):
-    """The default occupancy depends on the launch's size (W6 for the whole frame of C, W5 for an
-    8-way shard, kW6SamplesPerWave): the shard's rows must equal the same rows of the whole frame, bit
-    for bit, with RT_WAVES unset."""
+    """The default occupancy depends on the launch's size (fp32 runs at W5 below kW6PixelsPerWave pixels
+    per resident W6 wave, rt_common.hpp; the whole frame of C and its 8-way shards, ~42 pixels per W6
+    wave, both run at W6, so this checks the shard path's other work decomposition): the shard's rows must
+    equal the same rows of the whole frame, bit for bit, with RT_WAVES unset."""
     monkeypatch.delenv("RT_WAVES", raising=False)
     w, h, _, spp, depth = rt.scenes.CONFIGS["C"]
     flat = rt.scenes.config_scene("C").flatten()
@@ -212,8 +213,8 @@ def test_launch_size_rule_same_pixels(renderer, monkeypatch):
 
 
 def test_config_e_wave_builds(renderer, monkeypatch):
-    """The mega-level kernels at 5 (the fp32 default) and 6 waves, and the W4 kernel that sweeps the
-    same scene from the super boxes: one image, one segment count, the oracle's."""
+    """The mega-level kernels at 6 (the fp32 default, kWavesMegaF32) and 5 waves, and the W4 kernel that
+    sweeps the same scene from the super boxes: one image, one segment count, the oracle's."""
     flat = rt.scenes.config_scene("E").flatten()
     cam = cam_for(32, 18)
     _, lin_o, segs_o, _ = oracle_render(flat, cam, 50, 16, SEED, 0, precision="f32")
