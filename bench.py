@@ -19,6 +19,10 @@ roofline: the trace kernel is bound by VALU issue (no MFMA; HBM 
   blended by the FLOP mix; frac = achieved / peak <= 1.  The reference's brute-force work (17 FLOP
   per ray segment and sphere) is reported separately as brute_force_equiv: the culls
   skip most of it, so its "rate" exceeds the chip's peak and says how much work is avoided.
+  issue_frac: the VALU pipe's occupancy on a counter, 4 x (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / the
+  dispatch's SIMD-cycles (VALU quad-cycles, minus those in which two instructions issued together; 1.0 = the
+  pipe busy every cycle), and issue_frac_vs_ubench the same against the best VALU-saturating microbenchmark;
+  pmc_flop_frac: every FLOP the kernel executes (SQ_INSTS_VALU_FLOPS_FP32/64) at the vector peaks.
   valu_busy and traffic come from rocprofv3 PMC passes of this bench (profiles/pmc.json, with the
   commit and kernel-source hash they were collected at); when that hash is not the loaded library's
   (rt_version() "src=..."), they are reported as null and pmc_source.stale = true.
@@ -76,11 +80,13 @@ def pmc_fields(pmc, lib_src_hash, source_file):
     """roofline.traffic / valu_busy / pmc_source from a PMC record (tools/pmc_round.py).  The figures
     count only if they were collected from the kernel sources the loaded library was built from:
     otherwise (another hash, or a record without one) they are null and pmc_source.stale is true."""
+    keys = ("issue_frac", "issue_frac_vs_ubench", "pmc_flop_frac")
     if not pmc:
-        return {"traffic": None, "valu_busy": None, "pmc_source": None}
+        return {"traffic": None, "valu_busy": None, **{k: None for k in keys}, "pmc_source": None}
     stale = pmc.get("src_hash") is None or pmc.get("src_hash") != lib_src_hash
     return {"traffic": None if stale else pmc.get("hbm_bytes_per_launch"),
             "valu_busy": None if stale else pmc.get("valu_busy"),
+            **{k: (None if stale else pmc.get(k)) for k in keys},
             "pmc_source": {"file": source_file, "commit": pmc.get("commit"), "src_hash": pmc.get("src_hash"),
                            "library_src_hash": lib_src_hash, "stale": stale, "launch_ms": pmc.get("launch_ms")}}
 

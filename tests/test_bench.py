@@ -46,12 +46,16 @@ def test_world_size_mismatch_exits_nonzero():
 def test_pmc_record_from_other_sources_is_stale():
     b = _bench_module()
     rec = {"hbm_bytes_per_launch": 4.7e10, "valu_busy": 0.63, "commit": "656c11f74452", "src_hash": "aaaaaaaaaaaa",
-           "launch_ms": 39.5}
+           "launch_ms": 39.5, "issue_frac": 0.91, "issue_frac_vs_ubench": 1.01, "pmc_flop_frac": 0.27}
     f = b.pmc_fields(rec, "bbbbbbbbbbbb", "profiles/pmc.json")
     assert f["pmc_source"]["stale"] is True and f["traffic"] is None and f["valu_busy"] is None
+    assert f["issue_frac"] is None and f["pmc_flop_frac"] is None
     f = b.pmc_fields(rec, "aaaaaaaaaaaa", "profiles/pmc.json")
     assert f["pmc_source"]["stale"] is False and f["traffic"] == 4.7e10 and f["valu_busy"] == 0.63
+    assert f["issue_frac"] == 0.91 and f["issue_frac_vs_ubench"] == 1.01 and f["pmc_flop_frac"] == 0.27
     old = dict(rec)
     del old["src_hash"]   # a record written before the hash existed
     assert b.pmc_fields(old, "aaaaaaaaaaaa", "x")["pmc_source"]["stale"] is True
-    assert b.pmc_fields({}, "aaaaaaaaaaaa", "x") == {"traffic": None, "valu_busy": None, "pmc_source": None}
+    assert b.pmc_fields({}, "aaaaaaaaaaaa", "x") == {"traffic": None, "valu_busy": None, "issue_frac": None,
+                                                     "issue_frac_vs_ubench": None, "pmc_flop_frac": None,
+                                                     "pmc_source": None}

@@ -97,5 +97,32 @@ if ub:
             rec[f"valu_busy_vs_{k}"] = (rec["valu_active_per_simd_cycle_raw"] / cu) / (
                 cal[k]["insts_per_simd_cycle"] / cal[k]["cu_busy"])
     rec["valu_busy"] = rec.get("valu_busy_vs_f32")
+# Issue occupancy on a counter (round 6).  SQ_ACTIVE_INST_VALU counts VALU quad-cycles (1 per instruction, 2 per
+# fp32 transcendental, 4 per fp64 one) and SQ_ACTIVE_INST_VALU2 the quad-cycles in which two VALU instructions
+# issued together (fp32/int32 ops whose operands are all VGPRs: ~2 per quad-cycle; an SGPR or constant operand,
+# a packed, 64-bit, compare, select, cvt or 3-input op takes a quad-cycle alone: tools/ubench_bank2.hip).  So the
+# VALU pipe is busy 4 (ACTIVE - VALU2) SIMD-cycles; issue_frac is that over the dispatch's SIMD-cycles (1.0 = a
+# VALU quad-cycle in every 4 cycles of every SIMD), issue_frac_vs_ubench the same against ubench_valu's
+# independent FMA chains (8 waves per SIMD, nothing but VALU), the best rate measured on the chip.
+try:
+    iss = one("pmc_issue")
+except (AssertionError, KeyError):
+    iss = None
+if iss:
+    def quads(d):
+        return (d["SQ_ACTIVE_INST_VALU"] - d["SQ_ACTIVE_INST_VALU2"]) / (N_SIMD * d["GRBM_GUI_ACTIVE"] / 8.0)
+    rec["issue"] = {k: v for k, v in iss.items() if not k.startswith("_")}
+    rec["issue_frac"] = 4.0 * quads(iss)
+    rec["valu_dual_issue_share"] = 2.0 * iss["SQ_ACTIVE_INST_VALU2"] / iss["SQ_INSTS_VALU"]
+    rec["valu_lane_util"] = iss["SQ_THREAD_CYCLES_VALU"] / 64.0 / iss["SQ_INSTS_VALU"]
+    ubi = load("ubench_issue", lambda k: "chains" in k)
+    if ubi:
+        best = max(4.0 * quads(d) for d in ubi)
+        rec["issue_frac_ubench_best"] = best
+        rec["issue_frac_vs_ubench"] = rec["issue_frac"] / best
+# The PMC FLOP counters at the vector peaks (157.3 TF fp32, 78.6 TF fp64), over the PMC pass's own launch time:
+# every fp32/fp64 FLOP the kernel executes, where roofline.frac counts only the culls' and exact tests' FLOP.
+if "pmc_flop_fp32" in rec:
+    rec["pmc_flop_frac"] = (rec["pmc_flop_fp32"] / 157.3e12 + rec["pmc_flop_fp64"] / 78.6e12) / sq["_t"]
 json.dump({key: rec}, open(f"{out}/pmc.json", "w"), indent=1)
 print(json.dumps(rec, indent=1))

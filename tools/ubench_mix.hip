@@ -26,6 +26,14 @@ KIND(add_u32, uint32_t, "v_add_u32 %0, %1, %0", VC)
 KIND(bitop3, uint32_t, "v_bitop3_b32 %0, %1, %0, %1 bitop3:0x96", VC)
 KIND(cvt_f32_u32, float, "v_cvt_f32_u32 %0, %0", VC)
 KIND(cndmask, uint32_t, "v_cndmask_b32 %0, %1, %0, vcc", VC)
+KIND(mov_b32, uint32_t, "v_mov_b32 %0, %1", VC)
+KIND(and_b32, uint32_t, "v_and_b32 %0, %1, %0", VC)
+KIND(max3_f32, float, "v_max3_f32 %0, %1, %0, %0", VC)
+KIND(add_f32, float, "v_add_f32 %0, %1, %0", VC)
+KIND(pk_add_f32, f2, "v_pk_add_f32 %0, %1, %0", VC)
+KIND(pk_mul_f32, f2, "v_pk_mul_f32 %0, %1, %0", VC)
+KIND(fma_f64_abc, double, "v_fma_f64 %0, %1, %0, %0", VC)
+KIND(add_f64, double, "v_add_f64 %0, %1, %0", VC)
 
 struct fma_f32_abc {   // three distinct source registers (no repeated operand)
     typedef float type;
@@ -39,6 +47,13 @@ struct cndmask_s {   // the mask from an SGPR pair (e64), as the kernel's select
     static constexpr const char* name = "cndmask_sgpr";
     __device__ __forceinline__ static void op(uint32_t& x, uint32_t a) {
         asm volatile("v_cndmask_b32_e64 %0, %1, %0, %2" : "+v"(x) : "v"(a), "s"(0x5555555555555555ull));
+    }
+};
+struct cmp_e64 {   // a compare into an SGPR pair (the kernel's lane-mask compares)
+    typedef float type;
+    static constexpr const char* name = "cmp_e64";
+    __device__ __forceinline__ static void op(float& x, float a) {
+        asm volatile("v_cmp_gt_f32_e64 s[2:3], %0, %1" : "+v"(x) : "v"(a) : "s2", "s3");
     }
 };
 struct mad_u64 {
@@ -103,5 +118,14 @@ int main() {
     run<cndmask_s>(3u);
     run<fma_f32_abc>(0.999f);
     run<mad_u64>(3ull);
+    run<mov_b32>(3u);
+    run<and_b32>(3u);
+    run<max3_f32>(0.5f);
+    run<add_f32>(0.5f);
+    run<pk_add_f32>(f2{0.5f, 0.5f});
+    run<pk_mul_f32>(f2{0.999f, 0.999f});
+    run<fma_f64_abc>(0.999);
+    run<add_f64>(0.5);
+    run<cmp_e64>(0.5f);
     return 0;
 }
