@@ -6,7 +6,10 @@
 One step = one full frame of config C (1920x1080, 500 spheres, 512 spp, 50 bounces): every rank
 renders its row-interleaved shard (rows r, r+N, ...) with the HIP megakernel, then rank 0 gathers
 the RGB8 shards over RCCL and re-interleaves them (the north star's tiles + gather; total work is
-fixed as N grows -> "scaling": "strong").  Inputs (scene SoA, camera) are resident in HBM before
+fixed as N grows -> "scaling": "strong").  With RCCL the shards are double-buffered: frame k's gather
+is issued asynchronously and runs on RCCL's stream under frame k+1's render; frame k is assembled once
+its gather is done (--no-overlap: gather, then render the next frame).  The last frame's gather and
+assembly are inside the timed region.  Inputs (scene SoA, camera) are resident in HBM before
 the timed region.  Rank 0 prints one JSON line.  After the headline leg the same steps run in the
 other precision (fp64 = the reference's arithmetic when the headline is fp32), timed the same way,
 under the line's "f64" / "f32" key.
@@ -71,6 +74,10 @@ def parse():
                     help="static: rank r renders rows r, r+N, ... (one launch); dynamic: ranks pull row-interleaved "
                          "chunks from a shared queue (the reference's tile channel, renderer.rs:248-296)")
     ap.add_argument("--chunks", type=int, default=0, help="dynamic schedule: chunks per frame (0 = 4 x ranks)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="static schedule, nccl: gather each frame before the next render (no double buffering)")
+    ap.add_argument("--overlap-gloo", action="store_true",
+                    help="rehearsal: the double-buffered gather over gloo (host-staged shards), for one-GPU boxes")
     ap.add_argument("--probe-dist", action="store_true",
                     help="launcher rehearsal: set up the ranks and the process group, print the world, no GPU work")
     return ap.parse_args()
@@ -291,9 +298,20 @@ def main():
 
     from rt_mi355x import parallel
     tile = parallel.shard_range(W, H, world, rank)
+    # Two shard buffers (and two gather targets on rank 0): frame k+1 renders into the other buffer while frame k's
+    # RCCL gather is in flight (nccl: async gather on RCCL's own stream, waited only before frame k's assembly).
+    # --overlap-gloo (rehearsal on one GPU, where RCCL cannot run two ranks): the same pipeline over gloo, each
+    # rendered shard staged through a host buffer
+    pipelined = world > 1 and ((backend == "nccl" and not args.no_overlap) or (backend == "gloo" and args.overlap_gloo))
+    host_pipe = pipelined and backend != "nccl"
     shard = torch.zeros((parallel.rows_max(H, world), W, 3), dtype=torch.uint8, device="cuda")
     gathered = [torch.empty_like(shard) for _ in range(world)] if (world > 1 and rank == 0) else None
     image = torch.empty((H, W, 3), dtype=torch.uint8, device="cuda") if rank == 0 else None
+    pev = [None]   # the step's events while a pipelined gather completes (ev[2]: after the wait)
+    pimage = (image.cpu() if host_pipe else image) if rank == 0 else None
+    pipe = parallel.PipelinedGather(lambda: torch.zeros_like(shard, device="cpu" if host_pipe else "cuda"), world, rank,
+                                    H, pimage, after_wait=lambda: pev[0][2].record(stream) if pev[0] else None) \
+        if pipelined else None
     stream = torch.cuda.current_stream()
     sptr = ctypes.c_void_p(stream.cuda_stream)
     red_dev = "cuda" if backend == "nccl" else "cpu"
@@ -360,15 +378,35 @@ def main():
         if ev:
             ev[3].record(stream)
 
-    def step(flags, ev=None):
+    def flush():
+        """Complete the pipelined frame still in flight (its gather, then rank 0's assembly)."""
+        if pipe is not None:
+            pev[0] = None
+            pipe.flush()
+            if host_pipe and rank == 0:
+                image.copy_(pimage)
+
+    def step(flags, ev=None, k=0):
         if dynamic:
             return step_dynamic(flags, ev)
         if ev:
             ev[0].record(stream)
+        buf = pipe.buffer(k) if (pipe is not None and not host_pipe) else shard
         abi.check(lib, lib.rt_render_async(ctx, ctypes.byref(cam), depth, spp, args.seed, flags, ctypes.byref(tile),
-                                           ctypes.c_void_p(shard.data_ptr()), None, sptr))
+                                           ctypes.c_void_p(buf.data_ptr()), None, sptr))
         if ev:
             ev[1].record(stream)
+        if pipe is not None:
+            if host_pipe:
+                pipe.buffer(k).copy_(shard)   # synchronous staging (rehearsal only)
+            # frame k's gather starts once its render is done (RCCL's stream waits for this one) and runs under frame
+            # k+1's render; frame k-1's gather, issued under this render, is waited for and assembled now
+            pev[0] = ev
+            if pipe.submit(k) is None and ev:
+                ev[2].record(stream)
+            if ev:
+                ev[3].record(stream)
+            return
         if world > 1:
             if backend == "nccl":   # RCCL over xGMI, device buffers
                 dist.gather(shard, gathered, dst=0)
@@ -393,8 +431,9 @@ def main():
     def leg(precision):
         """Warm-up, then exactly args.steps timed steps between barriers; max over ranks."""
         flags = abi.RT_FLAG_F32 if precision == "f32" else 0
-        for _ in range(args.warmup):
-            step(flags)
+        for i in range(args.warmup):
+            step(flags, k=i)
+        flush()
         torch.cuda.synchronize()
         abi.check(lib, lib.rt_context_collect(ctx, sptr, ctypes.byref(abi.RtStats())), allow=(abi.RT_ERR_RANGE,))
         evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
@@ -405,7 +444,8 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            step(flags, evs[k])
+            step(flags, evs[k], k)
+        flush()   # the last frame's gather and assembly are inside the timed region
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -501,7 +541,8 @@ def main():
                                 + ((" + RCCL reduce" if backend == "nccl" else f" + {backend} reduce (rehearsal)")
                                    if world > 1 else "")) if dynamic else
                                (f"row-interleaved image shards x{world}"
-                                + ((" + RCCL gather" if backend == "nccl" else f" + {backend} gather (rehearsal)")
+                                + (((" + RCCL gather, double-buffered under the next frame's render" if pipelined
+                                     else " + RCCL gather") if backend == "nccl" else f" + {backend} gather (rehearsal)")
                                    if world > 1 else "")),
                 "schedule": args.schedule,
             },

@@ -87,3 +87,47 @@ def place_chunk(frame, chunk, height, n_chunks, j):
     nr = len(chunk_rows(height, n_chunks, j))
     frame[j::n_chunks] = chunk[:nr]
     return frame
+
+
+# ---- pipelined gather: frame k+1 renders while frame k's shards travel -----------------------------
+class PipelinedGather:
+    """Double-buffered row-shard gather to rank 0 (bench.py's static schedule over RCCL).
+
+    Frame k renders into buffer(k) (one of two shard buffers); submit(k) issues its gather asynchronously
+    (torch.distributed, async_op=True: RCCL runs it on its own stream after the render it depends on, gloo
+    in the background) and then completes frame k-1: waits for its gather -- with RCCL the current stream
+    waits, the host does not block -- and assembles it into `image` on rank 0.  So frame k's gather overlaps
+    frame k+1's render, and a buffer is rendered into again only after its previous gather completed.
+    flush() completes the frame still in flight.  Returns of submit/flush: the frame index assembled, or None.
+    The reference's renderer collects finished tiles on the main thread while workers keep rendering
+    (src/renderer.rs:300-365); this is the same overlap across GPUs."""
+
+    def __init__(self, make_buf, world, rank, height, image, after_wait=None):
+        self.world, self.rank, self.height, self.image = world, rank, height, image
+        self.bufs = [make_buf(), make_buf()]
+        self.gath = [[make_buf() for _ in range(world)] if rank == 0 else None for _ in range(2)]
+        self.after_wait = after_wait
+        self.pend = None
+
+    def buffer(self, k):
+        return self.bufs[k % 2]
+
+    def _finish(self, p):
+        w, g, k = p
+        w.wait()
+        if self.after_wait:
+            self.after_wait()
+        if self.rank == 0:
+            assemble_rows(g, self.height, self.world, self.image)
+        return k
+
+    def submit(self, k):
+        import torch.distributed as dist
+        g = self.gath[k % 2]
+        w = dist.gather(self.bufs[k % 2], g if self.rank == 0 else None, dst=0, async_op=True)
+        prev, self.pend = self.pend, (w, g, k)
+        return self._finish(prev) if prev else None
+
+    def flush(self):
+        prev, self.pend = self.pend, None
+        return self._finish(prev) if prev else None

@@ -140,3 +140,59 @@ def test_chunks_cover_every_row_once():
             rows = sorted(r for j in range(m) for r in parallel.chunk_rows(h, m, j))
             assert rows == list(range(h))
             assert all(parallel.chunk_range(17, h, m, j).row_count == len(parallel.chunk_rows(h, m, j)) for j in range(m))
+
+
+def _pipe_worker(rank, world, port, out_path, frames):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "rust-ray-tracing_amd"))
+    sys.path.insert(0, here)
+    import rt_mi355x as rt
+    from rt_mi355x import parallel
+    from oracle_bind import oracle_render
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
+    rows = list(parallel.shard_rows(H, world, rank))
+    pixels = np.array([r * W + c for r in rows for c in range(W)], np.uint32)
+    image = torch.zeros((H, W, 3), dtype=torch.float64) if rank == 0 else None
+    pipe = parallel.PipelinedGather(lambda: torch.zeros((parallel.rows_max(H, world), W, 3), dtype=torch.float64),
+                                    world, rank, H, image)
+    got = {}
+    for k in range(frames):   # frame k: seed SEED + k, rendered into the buffer frame k-2 used
+        _, lin, _, _ = oracle_render(flat, cam, DEPTH, SPP, SEED + k, pixels=pixels, threads=1)
+        buf = pipe.buffer(k)
+        buf.zero_()
+        buf[:len(rows)] = torch.from_numpy(lin.reshape(len(rows), W, 3))
+        done = pipe.submit(k)
+        assert done == (k - 1 if k > 0 else None)
+        if rank == 0 and done is not None:
+            got[done] = image.clone().numpy()
+    done = pipe.flush()
+    assert done == frames - 1 and pipe.flush() is None
+    if rank == 0:
+        got[done] = image.clone().numpy()
+        np.savez(out_path, **{f"f{k}": v for k, v in got.items()})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_gather_frames_bit_identical(tmp_path, world):
+    """bench.py's double-buffered gather (rt_mi355x.parallel.PipelinedGather): frame k renders while frame k-1's
+    async gather completes; every assembled frame (a different seed per frame, so a buffer mix-up would show)
+    equals the single-process render of that frame."""
+    out = str(tmp_path / "frames.npz")
+    frames = 4
+    mp.spawn(_pipe_worker, args=(world, _free_port(), out, frames), nprocs=world, join=True)
+    import rt_mi355x as rt
+    from oracle_bind import oracle_render
+    flat = rt.scenes.random_spheres(100).flatten()
+    cam = rt.camera_new_py(W, H, **rt.MAIN_CAMERA)
+    got = np.load(out)
+    assert sorted(got.files) == [f"f{k}" for k in range(frames)]
+    for k in range(frames):
+        _, full, _, _ = oracle_render(flat, cam, DEPTH, SPP, SEED + k)
+        np.testing.assert_array_equal(got[f"f{k}"], full.reshape(H, W, 3))

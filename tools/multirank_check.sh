@@ -26,16 +26,19 @@ RT_BENCH_SAVE=$OUT/singleC.npy timeout -k 10 200 python3 bench.py $ARGC > "$OUT/
 RT_BENCH_BACKEND=gloo RT_BENCH_SAVE=$OUT/self8.npy timeout -k 10 400 python3 bench.py --gpus 8 $ARGC > "$OUT/self8.log" 2>&1
 RT_BENCH_BACKEND=gloo RT_BENCH_SAVE=$OUT/dyn8.npy timeout -k 10 400 python3 bench.py --gpus 8 --schedule dynamic \
     $ARGC > "$OUT/dyn8.log" 2>&1
+# round 6: the double-buffered gather (parallel.PipelinedGather) in the real bench, 8 gloo ranks, host-staged
+RT_BENCH_BACKEND=gloo RT_BENCH_SAVE=$OUT/pipe8.npy timeout -k 10 400 python3 bench.py --gpus 8 --overlap-gloo \
+    --config C --steps 3 --warmup 1 --cpu-seconds 0 --other-precision 0 > "$OUT/pipe8.log" 2>&1
 python3 - "$OUT" <<'PY'
 import json, sys, numpy as np
 o = sys.argv[1]
-names = ("single", "nccl1", "gloo2", "self2", "dyn1", "dyn2", "singleC", "self8", "dyn8")
-a, b, c, d, e, f, g, h, i = (np.load(f"{o}/{n}.npy") for n in names)
+names = ("single", "nccl1", "gloo2", "self2", "dyn1", "dyn2", "singleC", "self8", "dyn8", "pipe8")
+a, b, c, d, e, f, g, h, i, j = (np.load(f"{o}/{n}.npy") for n in names)
 print("nccl world-1 identical:", np.array_equal(a, b), " gloo world-2 identical:", np.array_equal(a, c),
       " self-launched world-2 identical:", np.array_equal(a, d), " dynamic world-1 (nccl) identical:",
       np.array_equal(a, e), " dynamic world-2 (gloo) identical:", np.array_equal(a, f), a.shape)
 print("config C: self-launched world-8 identical:", np.array_equal(g, h), " dynamic world-8 identical:",
-      np.array_equal(g, i), g.shape)
+      np.array_equal(g, i), " pipelined gather world-8 identical:", np.array_equal(g, j), g.shape)
 for n in names:   # the decomposition rank 0 prints (bench.py "dist")
     line = json.loads([l for l in open(f"{o}/{n}.log") if l.startswith("{")][-1])
     dd = line["dist"]
@@ -45,5 +48,5 @@ for n in names:   # the decomposition rank 0 prints (bench.py "dist")
         print("   rank", r["rank"], "render_ms", r["render_ms"], "gather_ms", r["gather_ms"], "assemble_ms",
               r["assemble_ms"], "wall_s", r["wall_s"], "px_per_s", r["px_per_s"], "pixels", r.get("pixels"),
               "chunks", r.get("chunks"))
-assert all(np.array_equal(a, x) for x in (b, c, d, e, f)) and np.array_equal(g, h) and np.array_equal(g, i)
+assert all(np.array_equal(a, x) for x in (b, c, d, e, f)) and all(np.array_equal(g, x) for x in (h, i, j))
 PY
