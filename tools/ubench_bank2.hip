@@ -127,6 +127,36 @@ __global__ __launch_bounds__(256) void bank(float* out, int iters) {
 #define X(j) "v_mul_f32 v[64+2*" #j "], s20, v33\n"
                 R16(X) ::: CLOB);
 #undef X
+        if constexpr (K == 22)   // 32-bit integer multiply (the scratch records' slot offset)
+            asm volatile(
+#define X(j) "v_mul_lo_u32 v[64+2*" #j "], s20, v33\n"
+                R16(X) ::: CLOB);
+#undef X
+        if constexpr (K == 23)   // 64-bit shift-add (pointer arithmetic)
+            asm volatile(
+#define X(j) "v_lshl_add_u64 v[64+2*" #j ":65+2*" #j "], s[20:21], 0, v[32:33]\n"
+                R16(X) ::: CLOB);
+#undef X
+        if constexpr (K == 24)   // 24-bit multiply
+            asm volatile(
+#define X(j) "v_mul_u32_u24 v[64+2*" #j "], s20, v33\n"
+                R16(X) ::: CLOB);
+#undef X
+        if constexpr (K == 25)   // shift-or, all VGPRs
+            asm volatile(
+#define X(j) "v_lshl_or_b32 v[64+2*" #j "], v33, v34, v35\n"
+                R16(X) ::: CLOB);
+#undef X
+        if constexpr (K == 26)   // max, all VGPRs
+            asm volatile(
+#define X(j) "v_max_f32 v[64+2*" #j "], v33, v34\n"
+                R16(X) ::: CLOB);
+#undef X
+        if constexpr (K == 27)   // add_u32 with an SGPR
+            asm volatile(
+#define X(j) "v_add_u32 v[64+2*" #j "], s20, v33\n"
+                R16(X) ::: CLOB);
+#undef X
         if constexpr (K == 21)   // readfirstlane-free v_lshlrev (VOP2 shift)
             asm volatile(
 #define X(j) "v_lshlrev_b32 v[64+2*" #j "], 2, v33\n"
@@ -142,7 +172,8 @@ static const char* names[] = {"pk_fma s,v23,v01", "pk_fma s,v01,v01", "pk_fma s,
                               "pk_fma v01*v01+s", "pk_fma v01,v01,v01", "pk_mul s,v23", "fma s,v1,v2",
                               "fma s,v0,v0'", "max3 v1,v2,v3", "max3 v0,v0',v1", "max 0,v1", "fma v1,v2,v3",
                               "fma v1,v1',v2", "and_or v1,v2,v3", "sub v1,v2", "pk_add v01,v23", "pk_add v01,v01'",
-                              "cvt_f32_u32", "cndmask_e32 vcc", "mul s,v", "lshlrev 2,v"};
+                              "cvt_f32_u32", "cndmask_e32 vcc", "mul s,v", "lshlrev 2,v", "mul_lo_u32 s,v",
+                              "lshl_add_u64 s,0,v", "mul_u32_u24 s,v", "lshl_or v,v,v", "max v,v", "add_u32 s,v"};
 template <int K>
 static void run() {
     const int blocks = 256 * 8, threads = 256, iters = 8192;
@@ -167,6 +198,6 @@ static void run() {
 template <int... K> static void all(std::integer_sequence<int, K...>) { (run<K>(), ...); }
 int main() {
     for (int w = 0; w < 3; ++w) run<0>();
-    all(std::make_integer_sequence<int, 22>{});
+    all(std::make_integer_sequence<int, 28>{});
     return 0;
 }
