@@ -39,10 +39,13 @@ fi
 pass ubench_sq "$SQ" ./tools/bin/ubench_valu || exit 1
 pass ubench_issue "$ISSUE" ./tools/bin/ubench_valu || exit 1
 python3 tools/pmc_round.py "$OUT" "$CFG:$PREC:1" > "$OUT/pmc_summary.txt" 2>&1 || exit 1
-timeout -k 10 300 python3 bench.py --config "$CFG" --precision "$PREC" --steps 10 --warmup 2 --pmc "$OUT/pmc.json" \
+# LINE_ARGS: the bench line's steps (config E: --steps 3 --warmup 1 --cpu-seconds 0; its CPU baseline on 10 000
+# spheres outlasts the GPU box's silence limit)
+LINE_ARGS=${LINE_ARGS:---steps 10 --warmup 2}
+timeout -k 10 300 python3 bench.py --config "$CFG" --precision "$PREC" $LINE_ARGS --pmc "$OUT/pmc.json" \
     > "$OUT/bench.log" 2>&1 || exit 1
 grep '^{' "$OUT/bench.log" | tail -1 > "$OUT/bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/ktrace" -o run --output-format csv -- \
-    python3 bench.py --config "$CFG" --precision "$PREC" --steps 10 --warmup 2 --cpu-seconds 0 --other-precision 0 \
+    python3 bench.py --config "$CFG" --precision "$PREC" $LINE_ARGS --cpu-seconds 0 --other-precision 0 \
     --pmc "$OUT/pmc.json" > "$OUT/ktrace.log" 2>&1 || exit 1
 echo "profile_round done" >> "$OUT/status.txt"
