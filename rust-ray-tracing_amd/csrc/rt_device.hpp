@@ -86,7 +86,14 @@ __device__ __forceinline__ double sqrt_len(double x) {
     }
     return sqrt(x);
 }
-__device__ __forceinline__ float sqrt_len(float x) { return sqrtf(x); }
+// fp32: sqrt_nd when no lane holds a tiny positive argument (a wave ballot), else the library sqrtf -- the same
+// correctly rounded value.  The library sequence is ~16 VALU ops, most of them single-issue (compares, selects,
+// constant operands): unit() of every camera ray, the scatter's normal length and the hit test's sqrt(disc) take
+// the short form (round 6, same-box C fp32 +1.2 %, E +0.4 %: profiles/r06/sqrt_len_nd_ab.txt).
+__device__ __forceinline__ float sqrt_len(float x) {
+    if (__builtin_expect(__ballot(x > 0.0f && x < 0x1.0p-96f) == 0ull, 1)) return sqrt_nd(x);
+    return sqrtf(x);
+}
 template <typename T> __device__ __forceinline__ V3<T> neg(V3<T> a) { return mk(-a.x, -a.y, -a.z); }
 template <typename T> __device__ __forceinline__ T dot(V3<T> a, V3<T> b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 template <typename T> __device__ __forceinline__ T len2(V3<T> a) { return a.x * a.x + a.y * a.y + a.z * a.z; }
