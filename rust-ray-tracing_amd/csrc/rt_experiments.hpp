@@ -37,7 +37,10 @@ namespace rt {
 #ifdef RT_EXP_BLOCK_SAMPLES
 constexpr uint32_t kBlockSamples = RT_EXP_BLOCK_SAMPLES;
 #else
-constexpr uint32_t kBlockSamples = 8192;
+// 32768 (round 6; was 8192): config E (2048 spp, 1350 pixels per wave) takes G = 16 instead of 4, E fp32 +0.4 %,
+// fp64 +0.5 % same-box (profiles/r06/block_samples_ab.txt).  It changes G only where kBlockSamples / spp was the
+// binding bound; C (whole frame 8, row shards 2), D (4) and B keep theirs: the share bound decides for them
+constexpr uint32_t kBlockSamples = 32768;
 #endif
 #ifdef RT_EXP_TMUL
 constexpr uint32_t kTMul = RT_EXP_TMUL;
