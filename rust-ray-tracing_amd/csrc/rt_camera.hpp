@@ -141,8 +141,8 @@ __device__ __forceinline__ uint32_t cone_walk(const KP& q, float ax, float ay, f
 // The reference's exact test (objects.rs:252-257 on the camera-origin table) of sphere slot sl for the
 // camera rays of lanes v; the scene index (hit_update's tie rule and the result) comes with it.
 template <typename T, bool root2, bool SCALAR, typename KP>
-__device__ __forceinline__ void camera_exact(const KP& q, uint32_t sl, bool v, const V3<T>& d, T a, T inv_a, T& best_t,
-                                             int& best) {
+__device__ __forceinline__ void camera_exact(const KP& q, uint32_t sl, bool v, const V3<T>& d, T a, T inv_a,
+                                             HitBest<T>& bh) {
     KSTAT(2);
     constexpr bool kBothRoots = root2 || SCALAR;
     cptr<T> cxt = (cptr<T>)__builtin_assume_aligned(q.camx, 16);
@@ -159,7 +159,7 @@ __device__ __forceinline__ void camera_exact(const KP& q, uint32_t sl, bool v, c
             disc = fma(hb, hb, (-a) * c);
         }
         if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
-            hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best);
+            hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, bh);
     }
 }
 
@@ -202,18 +202,17 @@ __device__ __forceinline__ int camera_sweep(bool v, const V3<T>& d, T& t_out) {
     const float Cc = ufl(__builtin_amdgcn_sqrtf(__builtin_fmaf(-S, S, 1.0f)));
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
-    T best_t = T(INFINITY);
-    int best = -1;
+    HitBest<T> bh;
     KSTAT(3);
     uint32_t n_cx = 0;   // executed-work counts (work_add below)
     const uint32_t n_cone = cone_walk<MEGA>(q, ax, ay, az, S, Cc, all, xw0, kw0, [&](uint32_t sl) {
         ++n_cx;
-        camera_exact<T, root2, SCALAR>(q, sl, v, d, a, inv_a, best_t, best);
+        camera_exact<T, root2, SCALAR>(q, sl, v, d, a, inv_a, bh);
     });
     work_add(kWCone, n_cone);
     work_add(kWCExact, n_cx);
-    t_out = best_t;
-    return best;
+    t_out = bh.bt();
+    return bh.bi();
 }
 
 // Per-pixel camera candidate lists (camera batches): every primary ray of pixel (col, row) starts at
@@ -294,8 +293,7 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
     const auto& q = *cold_args<T>();
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254
-    T best_t = T(INFINITY);
-    int best = -1;
+    HitBest<T> bh;
     uint32_t n_cx = 0;
     // fp64: the whole list in one 16-byte LDS read (entries unpacked from SGPRs), and the next listed
     // sphere's camera-origin record and scene index requested while the current one is tested (C fp64
@@ -337,7 +335,7 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
                         disc = fma(hb, hb, (-a) * cur.c);
                     }
                     if (kBothRoots ? disc >= T(0.0) : (disc >= T(0.0) && hb <= T(0.0)))
-                        hit_update<T, root2, SCALAR>(hb, disc, cur.i, a, inv_a, best_t, best);
+                        hit_update<T, root2, SCALAR>(hb, disc, cur.i, a, inv_a, bh);
                 }
                 __builtin_amdgcn_s_waitcnt(0xC07F);
                 __builtin_amdgcn_sched_barrier(0);
@@ -350,13 +348,13 @@ __device__ __forceinline__ int camera_listed(bool v, const V3<T>& d, T& t_out, c
             const uint32_t n = __builtin_amdgcn_readfirstlane(l[0]);
             for (uint32_t j = 0; j < n; ++j) {
                 ++n_cx;
-                camera_exact<T, root2, SCALAR>(q, __builtin_amdgcn_readfirstlane(l[1u + j]), v, d, a, inv_a, best_t, best);
+                camera_exact<T, root2, SCALAR>(q, __builtin_amdgcn_readfirstlane(l[1u + j]), v, d, a, inv_a, bh);
             }
         }
     }
     work_add(kWCExact, n_cx);
-    t_out = best_t;
-    return best;
+    t_out = bh.bt();
+    return bh.bi();
 }
 
 // The per-lane "next ray" stage.  Fresh lanes run Camera::get_ray (ray_tracing.rs:77-89; jitter

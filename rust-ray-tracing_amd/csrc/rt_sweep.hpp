@@ -146,8 +146,32 @@ __device__ __forceinline__ uint32_t box_mask(const LBoxGroup& cur, f2 B0, f2 B1,
 // (objects.rs:227-234, ray_tracing.rs:231-235: the first minimum wins).  i is the scene index; ties
 // are broken by it (later wins, scalar: earlier wins), so the result does not depend on the order
 // in which spheres are visited (the general sweep visits them cluster by cluster).
+// The best hit so far (PackedHitRecords' t and sphere, objects.rs:121-155).  fp32: one 64-bit key
+// (bits(t) - bits(0.001f)) << 32 | ~index, the high half wrapping mod 2^32.  Non-negative floats order as their bits,
+// so "a smaller t, or the same t and a later sphere" (:141) is one unsigned 64-bit compare, and with the offset the
+// compare also holds the validity test (:272): a root below 0.001, -0, negative or NaN lands above every valid key,
+// and +inf meets the initial key (+inf, ~(-1) = 0) with ~index >= 1.  Round 6, same-box C fp32 +0.4 %, E +0.5 %
+// (profiles/r06/hit_key64_ab.txt): 5 compares, 4 SALU mask ops, a move and two selects became a subtract, a move,
+// one compare and two selects per candidate.
+template <typename T> struct HitBest {
+    T t = T(INFINITY);
+    int i = -1;
+    __device__ __forceinline__ T bt() const { return t; }
+    __device__ __forceinline__ int bi() const { return i; }
+    __device__ __forceinline__ void set(T r, uint32_t j) { t = r; i = (int)j; }
+};
+constexpr uint32_t kT001 = 0x3A83126Fu;   // bits of 0.001f (RN), the smallest valid root
+__device__ __forceinline__ uint64_t hit_key(float r, uint32_t j) {
+    return ((uint64_t)(__float_as_uint(r) - kT001) << 32) | (uint64_t)~j;
+}
+template <> struct HitBest<float> {
+    uint64_t k = (uint64_t)(0x7F800000u - kT001) << 32;
+    __device__ __forceinline__ float bt() const { return __uint_as_float((uint32_t)(k >> 32) + kT001); }
+    __device__ __forceinline__ int bi() const { return (int)~(uint32_t)k; }
+    __device__ __forceinline__ void set(float r, uint32_t j) { k = hit_key(r, j); }
+};
 template <typename T, bool root2, bool SCALAR>
-__device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_a, T& best_t, int& best) {
+__device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_a, HitBest<T>& bh) {
     if constexpr (SCALAR) {
         const T sd = sqrt(disc);
         T root = (-hb - sd) / a;
@@ -155,13 +179,19 @@ __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_
             root = (-hb + sd) / a;
             if (!(root >= T(0.001) && root < T(INFINITY))) return;
         }
-        if (root < best_t || (root == best_t && (int)i < best)) { best_t = root; best = (int)i; }   // first wins
+        if (root < bh.bt() || (root == bh.bt() && (int)i < bh.bi())) bh.set(root, i);   // first wins
         return;
     }
-    // fp64: the library sqrt's sequence without its range scaling when every candidate lane is in range
-    // (E fp64 +0.6 %); fp32: sqrtf
+    // sqrt_len: the library sqrt's sequence without its range scaling when every candidate lane is in range
+    // (fp64: E +0.6 %; fp32: round 6, with the other sqrt_len calls C +1.2 %)
     const T sd = sqrt_len(disc);
     const T r1 = (-hb - sd) * inv_a;                       // :270
+    if constexpr (sizeof(T) == 4 && !root2) {
+        // valid (:272) && better (:141) in one compare (HitBest<float>)
+        const uint64_t key = hit_key(r1, i);
+        bh.k = key < bh.k ? key : bh.k;
+        return;
+    }
     bool valid = r1 >= T(0.001) && r1 < T(INFINITY);       // :272
     T root = r1;
     if (root2 && !valid) {                                 // Q1 off: scalar semantics
@@ -170,22 +200,27 @@ __device__ __forceinline__ void hit_update(T hb, T disc, uint32_t i, T a, T inv_
     }
     // ties: later wins (:141); bitwise, so the update is two selects, not nested exec-mask branches (C fp32
     // +0.2 %, fp64 +1.3 %, E +0.4 % / +0.7 %: profiles/r05/hit_select_ab.txt)
-    const bool take = valid & ((root < best_t) | ((root == best_t) & ((int)i > best)));
-    best_t = take ? root : best_t;
-    best = take ? (int)i : best;
+    if constexpr (sizeof(T) == 4) {
+        const uint64_t key = hit_key(root, i);
+        const bool take = valid & (key < bh.k);
+        bh.k = take ? key : bh.k;
+    } else {
+        const bool take = valid & ((root < bh.t) | ((root == bh.t) & ((int)i > bh.i)));
+        bh.t = take ? root : bh.t;
+        bh.i = take ? (int)i : bh.i;
+    }
 }
 
 template <typename T, bool root2, bool SCALAR = false, bool CAMT = false, bool MEGA = false>
 __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, const V3<T>& d, T& t_out) {
     const T a = SCALAR ? len2(d) : pk_len2(d);       // objects.rs:219 / :253
     const T inv_a = SCALAR ? T(0) : T(1.0) / a;      // objects.rs:254 (loop-invariant)
-    T best_t = T(INFINITY);          // PackedHitRecords::default, objects.rs:128
-    int best = -1;
+    HitBest<T> bh;                   // PackedHitRecords::default, objects.rs:128
     // Sphere::hit_packed (objects.rs:249-290) + PackedHitRecords::update (objects.rs:140-155)
     // for a candidate whose discriminant is non-negative.  Exact pre-filter: with hb >= 0,
     // root1 = (-hb - sd)*inv_a <= 0 can never be valid, so only Q1-off (root2) mode needs it.
     KSTAT(CAMT ? 3 : 1);   // sweeps (one per wave)
-    auto hit = [&](T hb, T disc, uint32_t i) { hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, best_t, best); };
+    auto hit = [&](T hb, T disc, uint32_t i) { hit_update<T, root2, SCALAR>(hb, disc, i, a, inv_a, bh); };
     // Spheres stream through the scalar cache in 64-byte groups; group g+1 is requested before
     // group g is tested so the K$ latency hides behind the group's VALU work.
     // The buffer holds one extra dummy group, so the prefetch of group g+1 is always in bounds.
@@ -390,8 +425,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // sqrt(r2min), 1)): the margin factor folded into the host constant (box_cull_fuzz models this).
         // The best hit so far as a box-time bound (box_pair): fp64 rounds it up to a float.
         auto btf = [&]() -> float {
-            if constexpr (sizeof(T) == 4) return best_t;
-            else return (float)best_t * (1.0f + 0x1.0p-22f);   // RN(RN(b) (1 + 2^-22)) > b (b > 0)
+            if constexpr (sizeof(T) == 4) return bh.bt();
+            else return (float)bh.bt() * (1.0f + 0x1.0p-22f);   // RN(RN(b) (1 + 2^-22)) > b (b > 0)
         };
         const f2 nixy = {-ix, -iy}, aixy = {fabsf(ix), fabsf(iy)};
         const float aiz = fabsf(iz);
@@ -716,8 +751,8 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         work_add(kWFilt, n_filt);
         work_add(kWExact, n_exact);
     }
-    t_out = best_t;
-    return best;
+    t_out = bh.bt();
+    return bh.bi();
 }
 
 }  // namespace rt
