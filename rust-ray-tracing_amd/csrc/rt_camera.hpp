@@ -434,17 +434,17 @@ __device__ __forceinline__ void next_ray(bool cam, uint32_t colx, uint32_t rowy,
             nd = add(rv, nrm);
             if (near_zero(nd)) nd = nrm;
         } else {
-            nd = add(reflect(d, nrm), mul(rv, m.fuzz));
+            nd = add(reflect(d, nrm), mul(rv, m.p[3]));   // fuzz
         }
-        c = mk(c.x * m.ar, c.y * m.ag, c.z * m.ab);
+        c = mk(c.x * m.p[0], c.y * m.p[1], c.z * m.p[2]);   // albedo
     } else {
-        const T ratio = front ? m.inv_ior : m.ior;
+        const T ratio = front ? m.p[1] : m.p[0];   // 1/ior : ior
         const V3<T> nn = m.hollow ? neg(nrm) : nrm;
         const T ct = fmin(dot(neg(d), nn), T(1.0));
         const T st = sqrt_nd(T(1.0) - ct * ct);   // ct <= 1: 0, >= 2^-24 or negative
         bool refl = ratio * st > T(1.0);
         if (!refl) {   // Dielectric::reflectance (materials.rs:121-124), powi(5) = x*((x*x)*(x*x))
-            const T r0 = front ? m.r0_front : m.r0_back;
+            const T r0 = front ? m.p[2] : m.p[3];   // r0_front : r0_back
             const T m1 = T(1.0) - ct;
             const T m2 = m1 * m1;
             const T m5 = m1 * (m2 * m2);

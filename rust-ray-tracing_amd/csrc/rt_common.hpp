@@ -26,11 +26,11 @@ namespace rt {
 
 template <typename T> struct MatT {
     uint32_t kind, hollow;
-    T ar, ag, ab, fuzz, ior;
-    // Dielectric constants precomputed on the host in T with the reference's operations (IEEE,
-    // no contraction, so the bits equal the per-ray device computation): 1/ior (materials.rs:131)
-    // and Schlick's r0 = ((1-ratio)/(1+ratio))^2 (materials.rs:122) for ratio = 1/ior and ior.
-    T inv_ior, r0_front, r0_back;
+    // Lambertian / metal: {albedo r, g, b, fuzz}; dielectric: {ior, 1/ior, r0_front, r0_back} -- the constants
+    // precomputed on the host in T with the reference's operations (IEEE, no contraction, so the bits equal the
+    // per-ray device computation): 1/ior (materials.rs:131) and Schlick's r0 = ((1-ratio)/(1+ratio))^2
+    // (materials.rs:122) for ratio = 1/ior and ior.  Only the fields of the record's kind: fp64 40 bytes, fp32 24.
+    T p[4];
 };
 
 // Device sphere layout (rt_context_set_scene): 64-byte groups, one s_load_dwordx16 each, padded

@@ -41,8 +41,8 @@ static void pack_scene(const rt_scene* s, std::vector<T>& grp, std::vector<T>& c
         const T ior = (T)m.ior, one = T(1.0);
         const T inv = one / ior;
         const T qf = (one - inv) / (one + inv), qb = (one - ior) / (one + ior);
-        mats[i] = MatT<T>{m.kind, m.hollow, (T)m.albedo[0], (T)m.albedo[1], (T)m.albedo[2], (T)m.fuzz, ior,
-                          inv, qf * qf, qb * qb};
+        if (m.kind == RT_DIELECTRIC) mats[i] = MatT<T>{m.kind, m.hollow, {ior, inv, qf * qf, qb * qb}};
+        else mats[i] = MatT<T>{m.kind, m.hollow, {(T)m.albedo[0], (T)m.albedo[1], (T)m.albedo[2], (T)m.fuzz}};
     }
 }
 
