@@ -108,7 +108,6 @@ template <typename T> struct KParams {
     // n_xg leading groups of always-exact spheres, then cluster k at groups n_xg + 4k .. + 3
     const T* rsph;
     const float* rfsph;
-    const uint32_t* xrec;      // fp32: per slot group {r² of pair 0, r² of pair 1, 4 scene indices} (32 B)
     const float* ftop;
     const float* fsup;         // super boxes (4 clusters each), 4 per group
     const float* fmeg;         // mega boxes (4 supers each), 4 per group; n_mg groups, 0: no mega level

@@ -69,7 +69,6 @@ struct rt_context {
     void* cull64 = nullptr; void* cull32 = nullptr; // camera cone-cull records (fp32; rebuilt per launch)
     uint32_t n_cull = 0;                            // records: n_spheres rounded up to 64, + 64 padding
     void* rsph64 = nullptr; void* rsph32 = nullptr; // general sweep: slot-order exact groups
-    void* xrec32 = nullptr;                          // fp32: the exact test's r² and scene indices per group
     void* rfsph64 = nullptr; void* rfsph32 = nullptr; // slot-order fp32 filter groups
     void* top64 = nullptr; void* top32 = nullptr;   // cluster bounds (fp32 top groups)
     void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
@@ -180,8 +179,6 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->camx64); (void)hipFree(c->camx32); (void)hipFree(c->cull64); (void)hipFree(c->cull32);
     c->camx64 = c->camx32 = c->cull64 = c->cull32 = nullptr;
     (void)hipFree(c->rsph64); (void)hipFree(c->rsph32); (void)hipFree(c->rfsph64); (void)hipFree(c->rfsph32);
-    (void)hipFree(c->xrec32);
-    c->xrec32 = nullptr;
     (void)hipFree(c->top64); (void)hipFree(c->top32); (void)hipFree(c->ridx);
     (void)hipFree(c->sup64); (void)hipFree(c->sup32);
     c->sup64 = c->sup32 = nullptr;
@@ -345,21 +342,30 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->rsph64, rg64.data(), rg64.size() * sizeof(double))) != RT_OK) return rc;
         if ((rc = up(&c->rsph32, rg32.data(), rg32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->rfsph64, rf64.data(), rf64.size() * sizeof(float))) != RT_OK) return rc;
-        if ((rc = up(&c->rfsph32, rf32.data(), rf32.size() * sizeof(float))) != RT_OK) return rc;
+        {   // fp32: each cluster's 4 filter groups followed by their 4 exact records {r² of pair 0, r² of pair 1,
+            // 4 scene indices} (nearest_hit, exact4f): a walked group's centres are its filter group's (the same
+            // fp32 values), so a taken group loads only its 32-byte record, addressed from the loop's own pointer.
+            // The always-exact groups first, then 96 floats per cluster, then a dummy group (the loop's prefetch)
+            const size_t ngf = rf32.size() / 16 - 1, nxg = c->n_xg, ncl = (ngf - nxg) / 4;
+            std::vector<float> rx((size_t)16 * nxg + (size_t)96 * ncl + 32, 0.0f);
+            for (size_t g = 0; g < 16 * nxg; ++g) rx[g] = rf32[g];
+            for (size_t k = 0; k < ncl; ++k) {
+                float* b = &rx[16 * nxg + 96 * k];
+                for (size_t j = 0; j < 64; ++j) b[j] = rf32[16 * (nxg + 4 * k) + j];
+                for (size_t q = 0; q < 4; ++q) {
+                    const size_t g = nxg + 4 * k + q;
+                    uint32_t rec[8];
+                    for (int h = 0; h < 4; ++h) memcpy(&rec[h], &rg32[16 * g + 8 * (h / 2) + 6 + (h % 2)], 4);
+                    for (int j = 0; j < 4; ++j) rec[4 + j] = 4 * g + j < ridx.size() ? ridx[4 * g + j] : 0xFFFFFFFFu;
+                    memcpy(b + 64 + 8 * q, rec, 32);
+                }
+            }
+            for (size_t j = 0; j < 16; ++j) rx[16 * nxg + 96 * ncl + j] = rf32[16 * ngf + j];   // the dummy group
+            if ((rc = up(&c->rfsph32, rx.data(), rx.size() * sizeof(float))) != RT_OK) return rc;
+        }
         if ((rc = up(&c->top64, t64.data(), t64.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->top32, t32.data(), t32.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up((void**)&c->ridx, ridx.data(), ridx.size() * sizeof(uint32_t))) != RT_OK) return rc;
-        {   // fp32 exact-test records: a walked group's centres are its filter group's (the same fp32
-            // values), so a taken group loads only these 32 bytes (nearest_hit, exact4f)
-            const size_t ng = rg32.size() / 16;
-            std::vector<uint32_t> xr((size_t)8 * ng, 0xFFFFFFFFu);
-            for (size_t g = 0; g < ng; ++g) {
-                for (int q = 0; q < 2; ++q)
-                    for (int h = 0; h < 2; ++h) memcpy(&xr[8 * g + 2 * q + h], &rg32[16 * g + 8 * q + 6 + h], 4);
-                for (int j = 0; j < 4; ++j) if (4 * g + j < ridx.size()) xr[8 * g + 4 + j] = ridx[4 * g + j];
-            }
-            if ((rc = up((void**)&c->xrec32, xr.data(), xr.size() * sizeof(uint32_t))) != RT_OK) return rc;
-        }
         HIPCHK(hipMalloc(&c->camf64, f64g.size() * sizeof(float)));
         HIPCHK(hipMalloc(&c->camf32, f32g.size() * sizeof(float)));
     }
@@ -454,7 +460,6 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.n_fgroups = c->n_fgroups;
     p.rsph = (const T*)(f64 ? c->rsph64 : c->rsph32);
     p.rfsph = (const float*)(f64 ? c->rfsph64 : c->rfsph32);
-    p.xrec = f64 ? nullptr : (const uint32_t*)c->xrec32;
     p.ftop = (const float*)(f64 ? c->top64 : c->top32);
     p.fsup = (const float*)(f64 ? c->sup64 : c->sup32);
     p.fmeg = (const float*)(f64 ? c->meg64 : c->meg32);

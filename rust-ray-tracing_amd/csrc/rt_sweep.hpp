@@ -508,16 +508,16 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         };
         // fp32, scene-frame filter groups (not MEGA): the exact test of a taken group takes the centres
         // from its filter group, already in SGPRs (the same fp32 values, pack_filter / pack_sweep), and
-        // loads only the group's r² and scene indices (one s_load_dwordx8 instead of the 64-byte exact
-        // group plus the index table behind a kernel-argument load)
-        auto exact4f = [&](const SphGroup<float>& cur, uint32_t g, uint32_t pairs) {
+        // loads only the group's r² and scene indices: one s_load_dwordx8 from its record, which follows the
+        // cluster's filter groups in the same stream (round 6: a separate table behind a kernel-argument load
+        // cost two dependent scalar round trips per taken group; C fp32 +1.1 %, profiles/r06/xrec_inline_ab.txt)
+        auto exact4f = [&](const SphGroup<float>& cur, cptr<float> recp, uint32_t pairs) {
             KSTAT(0);
             if constexpr (sizeof(T) == 4) {
-                const auto& qx = *cold_args<T>();
-                cptr<uint32_t> xr = (cptr<uint32_t>)__builtin_assume_aligned(qx.xrec, 32);
+                cptr<uint32_t> xr = (cptr<uint32_t>)recp;
                 uint32_t rec[8];
 #pragma unroll
-                for (int j = 0; j < 8; ++j) rec[j] = xr[8u * g + (uint32_t)j];
+                for (int j = 0; j < 8; ++j) rec[j] = xr[(uint32_t)j];
                 const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
                 const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
                 const f2 na = {-a, -a};
@@ -611,7 +611,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     L3 = f2{-oe1l, -oe2l};
                     fg = (cptr<float>)__builtin_assume_aligned(ql.lfsph, 64);
                 }
-                sphere_loop(fg + 16u * g0, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
+                // fp32 scene-frame kernels: cluster kc's block in the filter stream is its 4 groups, then their
+                // 4 exact records (pack_sweep_inline)
+                constexpr bool kInl = sizeof(T) == 4 && !MEGA && !CAMT;
+                const cptr<float> fgb = kInl ? ff + 16u * nxg + 96u * kc : fg + 16u * g0;
+                sphere_loop(fgb, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                     uint32_t s0, s1;
                     // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
                     // rejects them as well (the filter passes every sphere the reference can hit).
@@ -632,7 +636,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                                     (__ballot(ps(Dv[1].x)) != 0ull ? 4u : 0u) | (__ballot(ps(Dv[1].y)) != 0ull ? 8u : 0u);
                             n_exact += (uint32_t)__builtin_popcount(pairs);
                         }
-                        if constexpr (sizeof(T) == 4 && !MEGA && !CAMT) exact4f(cur, g0 + g, pairs);
+                        if constexpr (kInl) exact4f(cur, fgb + 64u + 8u * g, pairs);
                         else
                             exact4(g0 + g, pairs);
                     }
