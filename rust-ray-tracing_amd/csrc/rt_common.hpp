@@ -115,7 +115,6 @@ template <typename T> struct KParams {
     // MEGA kernels: the sphere filter in cluster-local frames (pack_local): filter groups with centres
     // relative to their cluster's centre, and per cluster {Cx, Cy, Cz, Rc, r2max, 1/r2min, 0, 0}
     const float* lfsph;
-    const float* lclu;
     const float* lclb;         // ... the box levels in group-local frames (pack_local_boxes): per super its
     const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
     const float* lmeg;

@@ -74,7 +74,6 @@ struct rt_context {
     void* sup64 = nullptr; void* sup32 = nullptr;   // super boxes (4 clusters each)
     void* meg64 = nullptr; void* meg32 = nullptr;   // mega boxes (4 supers each; big scenes only)
     void* lfs64 = nullptr; void* lfs32 = nullptr;   // cluster-local filter groups (big scenes only)
-    void* lcl64 = nullptr; void* lcl32 = nullptr;   // ... and the per-cluster frame records
     void* lbx64[4] = {}; void* lbx32[4] = {};       // local box levels: cluster boxes, supers, megas, gigas
     uint32_t n_gg = 0;
     float l_r2max64 = 0, l_r2min64 = 0, l_r2max32 = 0, l_r2min32 = 0;
@@ -183,8 +182,8 @@ static void free_scene(rt_context* c) {
     (void)hipFree(c->sup64); (void)hipFree(c->sup32);
     c->sup64 = c->sup32 = nullptr;
     (void)hipFree(c->meg64); (void)hipFree(c->meg32);
-    (void)hipFree(c->lfs64); (void)hipFree(c->lfs32); (void)hipFree(c->lcl64); (void)hipFree(c->lcl32);
-    c->lfs64 = c->lfs32 = c->lcl64 = c->lcl32 = nullptr;
+    (void)hipFree(c->lfs64); (void)hipFree(c->lfs32);
+    c->lfs64 = c->lfs32 = nullptr;
     for (int lv = 0; lv < 4; ++lv) {
         (void)hipFree(c->lbx64[lv]); (void)hipFree(c->lbx32[lv]);
         c->lbx64[lv] = c->lbx32[lv] = nullptr;
@@ -254,6 +253,7 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if ((rc = up(&c->fsph32, f32g.data(), f32g.size() * sizeof(float))) != RT_OK) return rc;
         const SweepLayout L = build_layout(s);
         std::vector<double> rg64; std::vector<float> rg32, rf64, rf32, t64, t32, s64, s32, m64, m32;
+        std::vector<float> lf64, lf32, lr64, lr32;   // the mega kernels' local streams (uploaded inline below)
         pack_sweep(c64, fr64, L, rg64, rf64, t64, c->f_cmax64, c->f_r2max64, s64, m64);
         pack_sweep(c32, fr32, L, rg32, rf32, t32, c->f_cmax32, c->f_r2max32, s32, m32);
         if ((rc = up(&c->sup64, s64.data(), s64.size() * sizeof(float))) != RT_OK) return rc;
@@ -262,7 +262,7 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         if (c->n_mg) {
             if ((rc = up(&c->meg64, m64.data(), m64.size() * sizeof(float))) != RT_OK) return rc;
             if ((rc = up(&c->meg32, m32.data(), m32.size() * sizeof(float))) != RT_OK) return rc;
-            std::vector<float> lf64, lf32, lr64, lr32, q64, q32;
+            std::vector<float> q64, q32;
             pack_local(c64, L, t64, lf64, lr64, q64);
             pack_local(c32, L, t32, lf32, lr32, q32);
             std::vector<float> b64[4], b32[4];
@@ -280,10 +280,6 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
                 if ((rc = up(&c->lbx64[lv], b64[lv].data(), b64[lv].size() * sizeof(float))) != RT_OK) return rc;
                 if ((rc = up(&c->lbx32[lv], b32[lv].data(), b32[lv].size() * sizeof(float))) != RT_OK) return rc;
             }
-            if ((rc = up(&c->lfs64, lf64.data(), lf64.size() * sizeof(float))) != RT_OK) return rc;
-            if ((rc = up(&c->lfs32, lf32.data(), lf32.size() * sizeof(float))) != RT_OK) return rc;
-            if ((rc = up(&c->lcl64, lr64.data(), lr64.size() * sizeof(float))) != RT_OK) return rc;
-            if ((rc = up(&c->lcl32, lr32.data(), lr32.size() * sizeof(float))) != RT_OK) return rc;
         }
         c->n_top = (uint32_t)(L.members.size() / 4);
         c->n_xg = L.n_xg;
@@ -341,27 +337,40 @@ extern "C" int rt_context_set_scene(rt_context* c, const rt_scene* s) {
         HIPCHK(hipMalloc(&c->cullc32, cl32.size() / 4 * 4 * sizeof(float)));
         if ((rc = up(&c->rsph64, rg64.data(), rg64.size() * sizeof(double))) != RT_OK) return rc;
         if ((rc = up(&c->rsph32, rg32.data(), rg32.size() * sizeof(float))) != RT_OK) return rc;
-        if ((rc = up(&c->rfsph64, rf64.data(), rf64.size() * sizeof(float))) != RT_OK) return rc;
-        {   // fp32: each cluster's 4 filter groups followed by their 4 exact records {r² of pair 0, r² of pair 1,
-            // 4 scene indices} (nearest_hit, exact4f): a walked group's centres are its filter group's (the same
-            // fp32 values), so a taken group loads only its 32-byte record, addressed from the loop's own pointer.
-            // The always-exact groups first, then 96 floats per cluster, then a dummy group (the loop's prefetch)
-            const size_t ngf = rf32.size() / 16 - 1, nxg = c->n_xg, ncl = (ngf - nxg) / 4;
-            std::vector<float> rx((size_t)16 * nxg + (size_t)96 * ncl + 32, 0.0f);
-            for (size_t g = 0; g < 16 * nxg; ++g) rx[g] = rf32[g];
-            for (size_t k = 0; k < ncl; ++k) {
-                float* b = &rx[16 * nxg + 96 * k];
-                for (size_t j = 0; j < 64; ++j) b[j] = rf32[16 * (nxg + 4 * k) + j];
+        // General-sweep filter streams, inline layout (nearest_hit): the always-exact groups, then per cluster its 4
+        // filter groups, 4 records of 8 words {r^2 of pair 0 (2), r^2 of pair 1 (2), 4 scene indices} (r^2: the
+        // fp32 scene-frame stream, whose exact test takes the centres from the filter group; in the mega kernels'
+        // local streams the r^2 words of records 0 and 1 hold the cluster's frame record); then a dummy group (the
+        // loop's prefetch).  96 floats per cluster keep every group on its own 64-byte line.  A
+        // taken group's record and a walked cluster's frame are loads from the pointer the walk already holds.
+        auto inline_stream = [&](const std::vector<float>& src, bool r2, const std::vector<float>* frame) {
+            const size_t blk = 96, ngf = src.size() / 16 - 1, nxg = c->n_xg, nk = (ngf - nxg) / 4;
+            std::vector<float> rx((size_t)16 * nxg + blk * nk + 32, 0.0f);
+            for (size_t g = 0; g < 16 * nxg; ++g) rx[g] = src[g];
+            for (size_t k = 0; k < nk; ++k) {
+                float* b = &rx[16 * nxg + blk * k];
+                for (size_t j = 0; j < 64; ++j) b[j] = src[16 * (nxg + 4 * k) + j];
                 for (size_t q = 0; q < 4; ++q) {
                     const size_t g = nxg + 4 * k + q;
-                    uint32_t rec[8];
-                    for (int h = 0; h < 4; ++h) memcpy(&rec[h], &rg32[16 * g + 8 * (h / 2) + 6 + (h % 2)], 4);
+                    uint32_t rec[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+                    if (r2) for (int h = 0; h < 4; ++h) memcpy(&rec[h], &rg32[16 * g + 8 * (h / 2) + 6 + (h % 2)], 4);
                     for (int j = 0; j < 4; ++j) rec[4 + j] = 4 * g + j < ridx.size() ? ridx[4 * g + j] : 0xFFFFFFFFu;
                     memcpy(b + 64 + 8 * q, rec, 32);
                 }
+                if (frame) for (size_t j = 0; j < 4; ++j) { b[64 + j] = (*frame)[8 * k + j]; b[72 + j] = (*frame)[8 * k + 4 + j]; }
             }
-            for (size_t j = 0; j < 16; ++j) rx[16 * nxg + 96 * ncl + j] = rf32[16 * ngf + j];   // the dummy group
-            if ((rc = up(&c->rfsph32, rx.data(), rx.size() * sizeof(float))) != RT_OK) return rc;
+            for (size_t j = 0; j < 16; ++j) rx[16 * nxg + blk * nk + j] = src[16 * ngf + j];   // the dummy group
+            return rx;
+        };
+        {
+            const std::vector<float> rx32 = inline_stream(rf32, true, nullptr), rx64 = inline_stream(rf64, false, nullptr);
+            if ((rc = up(&c->rfsph32, rx32.data(), rx32.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->rfsph64, rx64.data(), rx64.size() * sizeof(float))) != RT_OK) return rc;
+        }
+        if (c->n_mg) {
+            const std::vector<float> lx32 = inline_stream(lf32, false, &lr32), lx64 = inline_stream(lf64, false, &lr64);
+            if ((rc = up(&c->lfs32, lx32.data(), lx32.size() * sizeof(float))) != RT_OK) return rc;
+            if ((rc = up(&c->lfs64, lx64.data(), lx64.size() * sizeof(float))) != RT_OK) return rc;
         }
         if ((rc = up(&c->top64, t64.data(), t64.size() * sizeof(float))) != RT_OK) return rc;
         if ((rc = up(&c->top32, t32.data(), t32.size() * sizeof(float))) != RT_OK) return rc;
@@ -465,7 +474,6 @@ static int launch_t(rt_context* c, const rt_camera* cam, uint32_t depth, uint32_
     p.fmeg = (const float*)(f64 ? c->meg64 : c->meg32);
     p.n_mg = c->n_mg;
     p.lfsph = (const float*)(f64 ? c->lfs64 : c->lfs32);
-    p.lclu = (const float*)(f64 ? c->lcl64 : c->lcl32);
     p.lclb = (const float*)(f64 ? c->lbx64[0] : c->lbx32[0]);
     p.lsup = (const float*)(f64 ? c->lbx64[1] : c->lbx32[1]);
     p.lmeg = (const float*)(f64 ? c->lbx64[2] : c->lbx32[2]);

@@ -370,7 +370,12 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         const auto& qa = *cold_args<T>();
         cptr<float> ff = (cptr<float>)__builtin_assume_aligned(qa.rfsph, 64);
         cptr<T> fe = (cptr<T>)__builtin_assume_aligned(qa.rsph, 64);
-        auto sidx = [&](uint32_t g) -> Q4 {   // scene indices of slot group g (one s_load_dwordx4)
+        // scene indices of slot group g: from the inline record ip (a walked cluster's group) or the slot table
+        auto sidx = [&](uint32_t g, cptr<float> ip) -> Q4 {
+            if (ip != nullptr) {
+                cptr<uint32_t> r = (cptr<uint32_t>)ip;
+                return Q4{r[0], r[1], r[2], r[3]};
+            }
             const auto& qi = *cold_args<T>();
             cptr<uint32_t> ri = (cptr<uint32_t>)__builtin_assume_aligned(qi.ridx, 16);
             return Q4{ri[4 * g], ri[4 * g + 1], ri[4 * g + 2], ri[4 * g + 3]};
@@ -453,7 +458,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
         // The exact test of spheres 4g..4g+3 (objects.rs:252-257; SCALAR: Sphere::hit :217-222), of
         // the sphere pairs set in `pairs` (fp32, bit q: spheres 4g+2q, 4g+2q+1; fp64, bit j: sphere
         // 4g+j; wave-uniform).
-        auto exact4 = [&](uint32_t g, uint32_t pairs = sizeof(T) == 4 ? 3u : 15u) {
+        auto exact4 = [&](uint32_t g, uint32_t pairs = sizeof(T) == 4 ? 3u : 15u, cptr<float> ip = nullptr) {
             KSTAT(0);
             if constexpr (sizeof(T) == 4) {
                 // Packed FP32: each v_pk_{add,mul,fma}_f32 evaluates the same IEEE op for two
@@ -462,7 +467,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                 const f2 ox = {o.x, o.x}, oy = {o.y, o.y}, oz = {o.z, o.z};
                 const f2 dx = {d.x, d.x}, dy = {d.y, d.y}, dz = {d.z, d.z};
                 const f2 na = {-a, -a};
-                const Q4 si = sidx(g);
+                const Q4 si = sidx(g, ip);
 #pragma unroll
                 for (uint32_t q = 0; q < 2; ++q) {
                     if (!((pairs >> q) & 1u)) continue;
@@ -499,7 +504,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         disc[j] = fma(hb[j], hb[j], -a * c);                   // :257
                     }
                 }
-                const Q4 si = sidx(g);
+                const Q4 si = sidx(g, ip);
                 const uint32_t sv[4] = {si.x, si.y, si.z, si.w};
 #pragma unroll
                 for (uint32_t j = 0; j < 4; ++j)
@@ -588,10 +593,12 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     // rounded), the margin from |o'|_1 and the cluster's Rc, r2max and 1/r2min, the
                     // basis scaled by it, and o' projected on the scaled basis.
                     const auto& ql = *cold_args<T>();
-                    cptr<float> lr = (cptr<float>)__builtin_assume_aligned(ql.lclu, 32);
-                    const f2 Ckxy = {lr[8u * kc], lr[8u * kc + 1u]};
-                    const float Ckz = lr[8u * kc + 2u];
-                    const float Rc = lr[8u * kc + 3u], r2x = lr[8u * kc + 4u], ir2 = lr[8u * kc + 5u];
+                    // the cluster's block in the local stream: 4 groups, then 4 records whose unused r^2 words
+                    // hold the frame {C_k, Rc} (record 0) and {r2max, 1/r2min} (record 1)
+                    fg = (cptr<float>)__builtin_assume_aligned(ql.lfsph, 64) + 16u * nxg + 96u * kc;
+                    const f2 Ckxy = {fg[64], fg[65]};
+                    const float Ckz = fg[66];
+                    const float Rc = fg[67], r2x = fg[72], ir2 = fg[73];
                     f2 opxy;
                     float opz;
                     if constexpr (sizeof(T) == 4) {
@@ -609,12 +616,11 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                     const float oe1l = __builtin_fmaf(opz, L0.y, opx * L0.x);
                     const float oe2l = __builtin_fmaf(opz, L2.x, __builtin_fmaf(opy, L1.y, opx * L1.x));
                     L3 = f2{-oe1l, -oe2l};
-                    fg = (cptr<float>)__builtin_assume_aligned(ql.lfsph, 64);
                 }
-                // fp32 scene-frame kernels: cluster kc's block in the filter stream is its 4 groups, then their
-                // 4 exact records (pack_sweep_inline)
+                // cluster kc's block in the filter stream: its 4 groups, then their 4 records (r^2 for the fp32
+                // scene-frame stream, the scene indices), then (mega streams) the frame record (inline_stream)
                 constexpr bool kInl = sizeof(T) == 4 && !MEGA && !CAMT;
-                const cptr<float> fgb = kInl ? ff + 16u * nxg + 96u * kc : fg + 16u * g0;
+                const cptr<float> fgb = MEGA ? fg : ff + 16u * nxg + 96u * kc;
                 sphere_loop(fgb, 4u, [&](const SphGroup<float>& cur, uint32_t g) {
                     uint32_t s0, s1;
                     // A wave-uniform branch: lanes the filter rejects run the exact test too, and it
@@ -638,7 +644,7 @@ __device__ __forceinline__ int nearest_hit(const KParams<T>& p, const V3<T>& o, 
                         }
                         if constexpr (kInl) exact4f(cur, fgb + 64u + 8u * g, pairs);
                         else
-                            exact4(g0 + g, pairs);
+                            exact4(g0 + g, pairs, fgb + 68u + 8u * g);
                     }
                 });
             }
