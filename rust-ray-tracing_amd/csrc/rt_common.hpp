@@ -107,13 +107,15 @@ template <typename T> struct KParams {
     // cluster bounds (fp32 groups of 4 {cx, cy, cz, R2}), slot -> scene index; n_top top groups,
     // n_xg leading groups of always-exact spheres, then cluster k at groups n_xg + 4k .. + 3
     const T* rsph;
-    const float* rfsph;
+    const float* rfsph;        // its fp32 filter groups, inline: cluster k's 4 groups at 16 n_xg + 96 k, then
+                               // their 4 records {r^2 of the pairs (fp32 rays), 4 scene indices} (inline_stream)
     const float* ftop;
     const float* fsup;         // super boxes (4 clusters each), 4 per group
     const float* fmeg;         // mega boxes (4 supers each), 4 per group; n_mg groups, 0: no mega level
     uint32_t n_mg;
     // MEGA kernels: the sphere filter in cluster-local frames (pack_local): filter groups with centres
-    // relative to their cluster's centre, and per cluster {Cx, Cy, Cz, Rc, r2max, 1/r2min, 0, 0}
+    // relative to their cluster's centre, inline with each cluster's records (set_scene's inline_stream: the
+    // scene indices, and the frame {Cx, Cy, Cz, Rc} / {r2max, 1/r2min} in the r^2 words of records 0 / 1)
     const float* lfsph;
     const float* lclb;         // ... the box levels in group-local frames (pack_local_boxes): per super its
     const float* lsup;         //     4 cluster boxes, per mega its 4 supers, per mega group its 4 megas
